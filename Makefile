@@ -1,0 +1,36 @@
+# Build librdeic_hip.so (HIP kernels for gfx950 + host C++ coders) in-tree.
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+BUILD := build
+LIBDIR := rdeic_amd/lib
+LIB := $(LIBDIR)/librdeic_hip.so
+HIP_SRCS := $(wildcard rdeic_amd/csrc/*.hip)
+CPP_SRCS := $(wildcard rdeic_amd/csrc/*.cpp)
+HIP_OBJS := $(patsubst rdeic_amd/csrc/%.hip,$(BUILD)/%.hip.o,$(HIP_SRCS))
+CPP_OBJS := $(patsubst rdeic_amd/csrc/%.cpp,$(BUILD)/%.cpp.o,$(CPP_SRCS))
+HIPFLAGS := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-variable -Wno-unused-but-set-variable
+CXXFLAGS := -O3 -fPIC -std=c++17 -Wall -pthread
+
+all: $(LIB) oracle
+
+$(BUILD)/%.hip.o: rdeic_amd/csrc/%.hip rdeic_amd/csrc/common.h include/rdeic_hip.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.cpp.o: rdeic_amd/csrc/%.cpp include/rdeic_hip.h
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS) $(CPP_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

@@ -1,0 +1,501 @@
+// Host entropy coders of the RDEIC bitstream, bit-compatible with the reference's
+// third-party natives (absent from the reference tree, restated from their published
+// algorithms; see DESIGN.md "Oracle"):
+//
+//  * compressai 1.2.4 rANS  — BufferedRansEncoder::encode_with_indexes / flush and
+//    RansDecoder::set_stream / decode_stream (called at model/compression.py:166,205-206,
+//    230-231 and utils/ckbd.py:103,112): ryg_rans 64-bit state, L = 2^31, 32-bit words,
+//    16-bit quantised CDFs, out-of-range values escaped through 4-bit "bypass" symbols.
+//  * compressai pmf_to_quantized_cdf (GaussianConditional.update, compression.py:275-280).
+//  * torchac 0.9.3 — 32-bit low/high binary arithmetic coder with pending (E3) bits, MSB-first
+//    bit packing, for the uniform 16384-symbol hyper-latent CDF (utils/ckbd.py:117-141).
+//
+// Differences by design: every export is reentrant (no global state) so images are coded on
+// independent host threads, and decoders bound every read — a truncated or corrupt stream
+// returns -EBADMSG instead of reading past the buffer (the reference treats any decompress
+// exception as a decode failure, experiments/run_robustness.py:277-297).
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/rdeic_hip.h"
+
+#define RDEIC_OK 0
+#define RDEIC_EINVAL (-22)
+#define RDEIC_ENOSPC (-28)
+#define RDEIC_EBADMSG (-74)
+
+namespace {
+
+constexpr int kPrecision = 16;
+constexpr uint32_t kBypassBits = 4;
+constexpr uint32_t kBypassMax = (1u << kBypassBits) - 1;
+constexpr uint64_t kRansL = 1ull << 31;
+
+struct RansSym {
+  uint16_t start;
+  uint16_t range;
+  bool bypass;
+};
+
+// ---- encoder --------------------------------------------------------------
+int rans_encode_impl(const int32_t* sym, const int32_t* idx, size_t n, const int32_t* cdf, int32_t cdf_ld,
+                     const int32_t* cdf_len, const int32_t* offset, int32_t levels, uint8_t* out, size_t cap,
+                     size_t* out_len, std::vector<RansSym>& syms, std::vector<uint32_t>& words) {
+  syms.clear();
+  syms.reserve(n + 16);
+  for (size_t i = 0; i < n; ++i) {
+    const int32_t ci = idx[i];
+    if (ci < 0 || ci >= levels) return RDEIC_EINVAL;
+    const int32_t* row = cdf + (size_t)ci * cdf_ld;
+    const int32_t max_value = cdf_len[ci] - 2;
+    if (max_value < 0 || max_value + 1 >= cdf_ld) return RDEIC_EINVAL;
+    int32_t value = sym[i] - offset[ci];
+    uint32_t raw = 0;
+    if (value < 0) {
+      raw = (uint32_t)(-2 * (int64_t)value - 1);
+      value = max_value;
+    } else if (value >= max_value) {
+      raw = (uint32_t)(2 * (int64_t)(value - max_value));
+      value = max_value;
+    }
+    syms.push_back({(uint16_t)row[value], (uint16_t)(row[value + 1] - row[value]), false});
+    if (value == max_value) {
+      int32_t nb = 0;
+      while (nb < 8 && (raw >> (nb * kBypassBits)) != 0) ++nb;
+      int32_t v = nb;
+      while (v >= (int32_t)kBypassMax) {
+        syms.push_back({(uint16_t)kBypassMax, (uint16_t)(kBypassMax + 1), true});
+        v -= kBypassMax;
+      }
+      syms.push_back({(uint16_t)v, (uint16_t)(v + 1), true});
+      for (int32_t j = 0; j < nb; ++j) {
+        uint32_t nib = (raw >> (j * kBypassBits)) & kBypassMax;
+        syms.push_back({(uint16_t)nib, (uint16_t)(nib + 1), true});
+      }
+    }
+  }
+  // flush: encode in reverse into a word buffer filled from the end
+  words.assign(syms.size() + 2, 0u);
+  size_t wp = words.size();
+  uint64_t x = kRansL;
+  for (size_t k = syms.size(); k-- > 0;) {
+    const RansSym& s = syms[k];
+    if (!s.bypass) {
+      const uint64_t freq = s.range;
+      const uint64_t x_max = ((kRansL >> kPrecision) << 32) * freq;
+      if (x >= x_max) {
+        words[--wp] = (uint32_t)x;
+        x >>= 32;
+      }
+      x = ((x / freq) << kPrecision) + (x % freq) + s.start;
+    } else {
+      const uint64_t freq = 1ull << (kPrecision - kBypassBits);
+      const uint64_t x_max = ((kRansL >> kPrecision) << 32) * freq;
+      if (x >= x_max) {
+        words[--wp] = (uint32_t)x;
+        x >>= 32;
+      }
+      x = (x << kBypassBits) | s.start;
+    }
+  }
+  words[--wp] = (uint32_t)(x >> 32);
+  words[--wp] = (uint32_t)x;
+  // after the two decrements, words[wp] = low half, words[wp+1] = high half
+  const size_t nbytes = (words.size() - wp) * 4;
+  *out_len = nbytes;
+  if (nbytes > cap) return RDEIC_ENOSPC;
+  memcpy(out, words.data() + wp, nbytes);
+  return RDEIC_OK;
+}
+
+// ---- decoder --------------------------------------------------------------
+struct RansDecoder {
+  std::vector<uint32_t> words;
+  size_t pos = 0;
+  uint64_t x = 0;
+  bool bad = false;
+
+  bool read_word(uint32_t& w) {
+    if (pos >= words.size()) { bad = true; return false; }
+    w = words[pos++];
+    return true;
+  }
+  uint32_t get_bits(uint32_t nbits) {
+    uint32_t v = (uint32_t)(x & ((1u << nbits) - 1));
+    x >>= nbits;
+    if (x < kRansL) {
+      uint32_t w;
+      if (read_word(w)) x = (x << 32) | w;
+    }
+    return v;
+  }
+};
+
+int rans_decode_impl(RansDecoder* d, const int32_t* idx, size_t n, const int32_t* cdf, int32_t cdf_ld,
+                     const int32_t* cdf_len, const int32_t* offset, int32_t levels, int32_t* out) {
+  if (d->bad) return RDEIC_EBADMSG;
+  for (size_t i = 0; i < n; ++i) {
+    const int32_t ci = idx[i];
+    if (ci < 0 || ci >= levels) return RDEIC_EINVAL;
+    const int32_t* row = cdf + (size_t)ci * cdf_ld;
+    const int32_t len = cdf_len[ci];
+    const int32_t max_value = len - 2;
+    if (max_value < 0 || len > cdf_ld) return RDEIC_EINVAL;
+    const uint32_t cum = (uint32_t)(d->x & ((1u << kPrecision) - 1));
+    // first entry > cum, minus one (rows are strictly increasing; row[len-1] = 2^16 > cum)
+    const int32_t* it = std::upper_bound(row, row + len, (int32_t)cum);
+    int32_t s = (int32_t)(it - row) - 1;
+    if (s < 0 || s >= len - 1) return RDEIC_EBADMSG;
+    const uint64_t start = (uint32_t)row[s], freq = (uint32_t)(row[s + 1] - row[s]);
+    uint64_t x = d->x;
+    x = freq * (x >> kPrecision) + (x & ((1u << kPrecision) - 1)) - start;
+    if (x < kRansL) {
+      uint32_t w;
+      if (!d->read_word(w)) return RDEIC_EBADMSG;
+      x = (x << 32) | w;
+    }
+    d->x = x;
+    int32_t value = s;
+    if (value == max_value) {
+      int32_t v = (int32_t)d->get_bits(kBypassBits);
+      int32_t nb = v;
+      while (v == (int32_t)kBypassMax) {
+        if (d->bad || nb > 8) return RDEIC_EBADMSG;
+        v = (int32_t)d->get_bits(kBypassBits);
+        nb += v;
+      }
+      if (nb > 8) return RDEIC_EBADMSG;
+      uint32_t raw = 0;
+      for (int32_t j = 0; j < nb; ++j) {
+        uint32_t nib = d->get_bits(kBypassBits);
+        raw |= nib << (j * kBypassBits);
+      }
+      if (d->bad) return RDEIC_EBADMSG;
+      value = (int32_t)(raw >> 1);
+      if (raw & 1)
+        value = -value - 1;
+      else
+        value += max_value;
+    }
+    out[i] = value + offset[ci];
+  }
+  return d->bad ? RDEIC_EBADMSG : RDEIC_OK;
+}
+
+template <typename F>
+void parallel_for(int32_t count, int32_t threads, F&& f) {
+  if (threads <= 1 || count <= 1) {
+    for (int32_t i = 0; i < count; ++i) f(i);
+    return;
+  }
+  threads = std::min(threads, count);
+  std::atomic<int32_t> next{0};
+  std::vector<std::thread> pool;
+  pool.reserve(threads);
+  for (int32_t t = 0; t < threads; ++t)
+    pool.emplace_back([&]() {
+      for (;;) {
+        int32_t i = next.fetch_add(1);
+        if (i >= count) break;
+        f(i);
+      }
+    });
+  for (auto& th : pool) th.join();
+}
+
+// ---- torchac-compatible arithmetic coder ------------------------------------
+struct BitWriter {
+  uint8_t* out;
+  size_t cap;
+  size_t len = 0;
+  uint8_t cache = 0;
+  int count = 0;
+  bool overflow = false;
+  void put(int bit) {
+    cache = (uint8_t)((cache << 1) | (bit & 1));
+    if (++count == 8) {
+      if (len < cap) out[len] = cache; else overflow = true;
+      ++len;
+      count = 0;
+      cache = 0;
+    }
+  }
+  void put_with_pending(int bit, uint64_t& pending) {
+    put(bit);
+    while (pending > 0) { put(!bit); --pending; }
+  }
+  void flush() {
+    while (count > 0) put(0);
+  }
+};
+
+struct BitReader {
+  const uint8_t* in;
+  size_t n;
+  size_t ptr = 0;
+  uint8_t cache = 0;
+  int cached = 0;
+  void get(uint32_t& value) {
+    if (cached == 0) {
+      if (ptr == n) { value <<= 1; return; }  // torchac shifts in zeros past the end
+      cache = in[ptr++];
+      cached = 8;
+    }
+    value = (value << 1) | ((cache >> (cached - 1)) & 1);
+    --cached;
+  }
+};
+
+inline uint16_t binsearch_u16(const uint16_t* cdf, uint16_t target, uint16_t max_sym) {
+  uint16_t left = 0, right = (uint16_t)(max_sym + 1);
+  while (left + 1 < right) {
+    const uint16_t m = (uint16_t)((left + right) / 2);
+    const uint16_t v = cdf[m];
+    if (v < target) left = m;
+    else if (v > target) right = m;
+    else return m;
+  }
+  return left;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rdeic_version(void) { return 1; }
+
+// number of entry points declared in include/rdeic_hip.h (checked by tests/test_abi.py)
+int rdeic_abi_count(void) { return 39; }
+
+int rdeic_pmf_to_quantized_cdf(const float* pmf, int32_t n, int32_t precision, uint32_t* cdf_out) {
+  if (!pmf || !cdf_out || n <= 0 || precision <= 0 || precision > 24) return RDEIC_EINVAL;
+  for (int32_t i = 0; i < n; ++i)
+    if (!(pmf[i] >= 0.f) || !std::isfinite(pmf[i])) return RDEIC_EINVAL;
+  const uint32_t one = 1u << precision;
+  std::vector<uint32_t> cdf((size_t)n + 1);
+  cdf[0] = 0;
+  for (int32_t i = 0; i < n; ++i) cdf[i + 1] = (uint32_t)std::round(pmf[i] * (float)one);
+  uint64_t total = 0;
+  for (uint32_t v : cdf) total += v;
+  if (total == 0) return RDEIC_EINVAL;
+  for (auto& v : cdf) v = (uint32_t)(((uint64_t)one * v) / total);
+  for (size_t i = 1; i < cdf.size(); ++i) cdf[i] += cdf[i - 1];
+  cdf.back() = one;
+  const int32_t m = (int32_t)cdf.size();
+  for (int32_t i = 0; i < m - 1; ++i) {
+    if (cdf[i] == cdf[i + 1]) {
+      uint32_t best_freq = ~0u;
+      int32_t best = -1;
+      for (int32_t j = 0; j < m - 1; ++j) {
+        const uint32_t f = cdf[j + 1] - cdf[j];
+        if (f > 1 && f < best_freq) { best_freq = f; best = j; }
+      }
+      if (best < 0) return RDEIC_EINVAL;
+      if (best < i) {
+        for (int32_t j = best + 1; j <= i; ++j) cdf[j]--;
+      } else {
+        for (int32_t j = i + 1; j <= best; ++j) cdf[j]++;
+      }
+    }
+  }
+  memcpy(cdf_out, cdf.data(), cdf.size() * sizeof(uint32_t));
+  return RDEIC_OK;
+}
+
+int rdeic_build_gaussian_tables(const float* pmf, const int32_t* pmf_len, int32_t levels, int32_t pmf_ld, int32_t* cdf,
+                                int32_t cdf_ld, int32_t* cdf_len, void* reserved) {
+  (void)reserved;
+  if (!pmf || !pmf_len || !cdf || !cdf_len || levels <= 0) return RDEIC_EINVAL;
+  std::vector<float> row;
+  std::vector<uint32_t> q;
+  for (int32_t i = 0; i < levels; ++i) {
+    const int32_t L = pmf_len[i];
+    if (L <= 0 || L + 1 > pmf_ld || L + 2 > cdf_ld) return RDEIC_EINVAL;
+    // pmf row: L probabilities followed by the tail mass at column L
+    row.assign(pmf + (size_t)i * pmf_ld, pmf + (size_t)i * pmf_ld + L + 1);
+    q.assign((size_t)L + 2, 0u);
+    int rc = rdeic_pmf_to_quantized_cdf(row.data(), L + 1, kPrecision, q.data());
+    if (rc) return rc;
+    int32_t* out = cdf + (size_t)i * cdf_ld;
+    for (int32_t j = 0; j < cdf_ld; ++j) out[j] = j < L + 2 ? (int32_t)q[j] : 0;
+    cdf_len[i] = L + 2;
+  }
+  return RDEIC_OK;
+}
+
+int rdeic_rans_encode(const int32_t* sym, const int32_t* idx, size_t n, const int32_t* cdf, int32_t cdf_ld,
+                      const int32_t* cdf_len, const int32_t* offset, int32_t levels, uint8_t* out, size_t cap,
+                      size_t* out_len) {
+  if ((!sym || !idx) && n) return RDEIC_EINVAL;
+  if (!cdf || !cdf_len || !offset || !out || !out_len || levels <= 0) return RDEIC_EINVAL;
+  try {
+    std::vector<RansSym> syms;
+    std::vector<uint32_t> words;
+    return rans_encode_impl(sym, idx, n, cdf, cdf_ld, cdf_len, offset, levels, out, cap, out_len, syms, words);
+  } catch (const std::bad_alloc&) {
+    return RDEIC_ENOSPC;
+  }
+}
+
+int rdeic_rans_encode_batch(int32_t count, const int32_t* sym, const int32_t* idx, size_t n_per, size_t stride,
+                            const int32_t* cdf, int32_t cdf_ld, const int32_t* cdf_len, const int32_t* offset,
+                            int32_t levels, uint8_t* out, size_t cap_per, size_t* out_len, int32_t threads) {
+  if (count <= 0 || !sym || !idx || !out || !out_len) return RDEIC_EINVAL;
+  std::vector<int> rc(count, 0);
+  parallel_for(count, threads, [&](int32_t i) {
+    try {
+      std::vector<RansSym> syms;
+      std::vector<uint32_t> words;
+      rc[i] = rans_encode_impl(sym + i * stride, idx + i * stride, n_per, cdf, cdf_ld, cdf_len, offset, levels,
+                               out + i * cap_per, cap_per, &out_len[i], syms, words);
+    } catch (const std::bad_alloc&) {
+      rc[i] = RDEIC_ENOSPC;
+    }
+  });
+  for (int v : rc)
+    if (v) return v;
+  return RDEIC_OK;
+}
+
+void* rdeic_rans_dec_open(const uint8_t* data, size_t len) {
+  if (!data && len) return nullptr;
+  RansDecoder* d = new (std::nothrow) RansDecoder();
+  if (!d) return nullptr;
+  const size_t nw = len / 4;
+  d->words.resize(nw);
+  if (nw) memcpy(d->words.data(), data, nw * 4);
+  if (len % 4 != 0 || nw < 2) {
+    d->bad = true;
+    return d;
+  }
+  d->x = (uint64_t)d->words[0] | ((uint64_t)d->words[1] << 32);
+  d->pos = 2;
+  return d;
+}
+
+int rdeic_rans_decode(void* handle, const int32_t* idx, size_t n, const int32_t* cdf, int32_t cdf_ld,
+                      const int32_t* cdf_len, const int32_t* offset, int32_t levels, int32_t* out) {
+  if (!handle || (!idx && n) || (!out && n) || !cdf || !cdf_len || !offset) return RDEIC_EINVAL;
+  return rans_decode_impl((RansDecoder*)handle, idx, n, cdf, cdf_ld, cdf_len, offset, levels, out);
+}
+
+int rdeic_rans_decode_batch(int32_t count, void** handles, const int32_t* idx, size_t n_per, size_t stride,
+                            const int32_t* cdf, int32_t cdf_ld, const int32_t* cdf_len, const int32_t* offset,
+                            int32_t levels, int32_t* out, int32_t threads) {
+  if (count <= 0 || !handles || !idx || !out) return RDEIC_EINVAL;
+  std::vector<int> rc(count, 0);
+  parallel_for(count, threads, [&](int32_t i) {
+    rc[i] = handles[i] ? rans_decode_impl((RansDecoder*)handles[i], idx + i * stride, n_per, cdf, cdf_ld, cdf_len,
+                                          offset, levels, out + i * stride)
+                       : RDEIC_EINVAL;
+  });
+  for (int v : rc)
+    if (v) return v;
+  return RDEIC_OK;
+}
+
+void rdeic_rans_dec_close(void* handle) { delete (RansDecoder*)handle; }
+
+int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row) {
+  // compute_cdf_uniform_prob (utils/ckbd.py:117-128): float32 cumsum of 1/K, last = 1.0;
+  // torchac _convert_to_int_and_normalize: round(cdf * (2^16 - (Lp-1))) as int16, + arange(Lp).
+  if (codebook_size <= 0 || codebook_size > 32768 || !cdf_row) return RDEIC_EINVAL;
+  const int32_t lp = codebook_size + 1;
+  const float p = 1.0f / (float)codebook_size;
+  float acc = 0.f;
+  const float maxv = 65536.0f - (float)(lp - 1);
+  for (int32_t k = 0; k < lp; ++k) {
+    float c = (k == lp - 1) ? 1.0f : acc;
+    float v = std::nearbyint(c * maxv);
+    int32_t iv = (int32_t)v;
+    cdf_row[k] = (int16_t)(uint16_t)((uint32_t)(iv + k) & 0xFFFFu);
+    acc += p;
+  }
+  return RDEIC_OK;
+}
+
+int rdeic_ac_encode(const int16_t* sym, size_t n, const int16_t* cdf_row, int32_t lp, uint8_t* out, size_t cap,
+                    size_t* out_len) {
+  if ((!sym && n) || !cdf_row || lp < 2 || !out || !out_len) return RDEIC_EINVAL;
+  const uint16_t* cdf = (const uint16_t*)cdf_row;
+  const int32_t max_symbol = lp - 2;
+  BitWriter bw{out, cap};
+  uint32_t low = 0, high = 0xFFFFFFFFu;
+  uint64_t pending = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const int32_t s = sym[i];
+    if (s < 0 || s > max_symbol) return RDEIC_EINVAL;
+    const uint64_t span = (uint64_t)high - (uint64_t)low + 1;
+    const uint32_t c_low = cdf[s];
+    const uint32_t c_high = s == max_symbol ? 0x10000u : cdf[s + 1];
+    high = (low - 1) + (uint32_t)((span * c_high) >> kPrecision);
+    low = low + (uint32_t)((span * c_low) >> kPrecision);
+    for (;;) {
+      if (high < 0x80000000u) {
+        bw.put_with_pending(0, pending);
+        low <<= 1;
+        high = (high << 1) | 1;
+      } else if (low >= 0x80000000u) {
+        bw.put_with_pending(1, pending);
+        low <<= 1;
+        high = (high << 1) | 1;
+      } else if (low >= 0x40000000u && high < 0xC0000000u) {
+        ++pending;
+        low = (low << 1) & 0x7FFFFFFFu;
+        high = (high << 1) | 0x80000001u;
+      } else {
+        break;
+      }
+    }
+  }
+  pending += 1;
+  bw.put_with_pending(low < 0x40000000u ? 0 : 1, pending);
+  bw.flush();
+  *out_len = bw.len;
+  return bw.overflow ? RDEIC_ENOSPC : RDEIC_OK;
+}
+
+int rdeic_ac_decode(const uint8_t* data, size_t len, size_t n, const int16_t* cdf_row, int32_t lp, int16_t* out) {
+  if ((!data && len) || !cdf_row || lp < 2 || (!out && n)) return RDEIC_EINVAL;
+  if (n == 0) return RDEIC_OK;
+  const uint16_t* cdf = (const uint16_t*)cdf_row;
+  const uint16_t max_symbol = (uint16_t)(lp - 2);
+  BitReader br{data, len};
+  uint32_t low = 0, high = 0xFFFFFFFFu, value = 0;
+  for (int i = 0; i < 32; ++i) br.get(value);
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t span = (uint64_t)high - (uint64_t)low + 1;
+    const uint16_t count = (uint16_t)((((uint64_t)value - (uint64_t)low + 1) * 0x10000u - 1) / span);
+    const uint16_t s = binsearch_u16(cdf, count, max_symbol);
+    out[i] = (int16_t)s;
+    if (i == n - 1) break;
+    const uint32_t c_low = cdf[s];
+    const uint32_t c_high = s == max_symbol ? 0x10000u : cdf[s + 1];
+    high = (low - 1) + (uint32_t)((span * c_high) >> kPrecision);
+    low = low + (uint32_t)((span * c_low) >> kPrecision);
+    for (;;) {
+      if (low >= 0x80000000u || high < 0x80000000u) {
+        low <<= 1;
+        high = (high << 1) | 1;
+        br.get(value);
+      } else if (low >= 0x40000000u && high < 0xC0000000u) {
+        low = (low << 1) & 0x7FFFFFFFu;
+        high = (high << 1) | 0x80000001u;
+        value -= 0x40000000u;
+        br.get(value);  // get() shifts value left and appends the next bit
+      } else {
+        break;
+      }
+    }
+  }
+  return RDEIC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// Shared device helpers for the RDEIC MI355X (gfx950) kernels.
+//
+// Layout conventions used by every kernel in this library:
+//   * activations are NHWC ("pixel-major, channel-contiguous"); a tensor is
+//     addressed as base + pixel * ld + channel, where ld >= C lets a kernel
+//     read or write a channel slice of a wider buffer (this is how the
+//     reference's torch.cat / channel slicing is expressed without copies);
+//   * conv / linear weights are packed once at load time as [Cout][KH][KW][Cin]
+//     (K-contiguous), so both GEMM operands of the implicit-GEMM conv are
+//     K-major and feed MFMA fragments with 16-byte loads;
+//   * "dtype" 0 = fp32 parity mode, 1 = bf16 perf mode (fp32 accumulate).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RDEIC_OK 0
+#define RDEIC_EINVAL (-22)
+#define RDEIC_ENOSPC (-28)
+#define RDEIC_EBADMSG (-74)
+#define RDEIC_ELAUNCH (-5)
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// exact-erf GELU (torch.nn.GELU / F.gelu default)
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? RDEIC_OK : RDEIC_ELAUNCH;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

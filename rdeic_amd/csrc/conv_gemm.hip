@@ -1,0 +1,375 @@
+// Implicit-GEMM convolution / linear for gfx950 (MFMA), NHWC activations.
+//
+// GEMM view: M = n*ho*wo output pixels, N = cout, K = kh*kw*cin.
+//   A[m, k] is gathered on the fly from NHWC input(s) (k = (ky, kx, ci), ci fastest)
+//   B[k, n] = packed weight [cout][wld] (K-contiguous rows)
+// Both operands are K-major in LDS, so an MFMA fragment (8 consecutive k of one
+// row for bf16 16x16x32, 1 element for f32 16x16x4) is one ds_read per lane.
+//
+// Fusions (all optional, selected per launch):
+//   prologue : two-segment channel concat (UNet skip concat, control-branch input),
+//              nearest x2 upsample (UNet/VAE Upsample), stride / asymmetric pad
+//              (UNet / VAE Downsample), GroupNorm affine + SiLU on the gathered values
+//   epilogue : bias, per-(image, cout) timestep-embedding add, activation
+//              (leaky_relu / gelu / silu), residual add, PixelShuffle(2) store.
+//
+// Accumulation order over K is fixed (k-tiles in order, fixed MFMA), independent of
+// tile shape or batch size, so results are batch-invariant — a requirement of the
+// entropy model (encoder and decoder must recompute identical means / scales).
+//
+// Replaces: every nn.Conv2d / nn.Linear on the RDEIC hot path (see include/rdeic_hip.h).
+#include "common.h"
+#include "../../include/rdeic_hip.h"
+
+namespace {
+
+struct ConvArgs {
+  const char* in0; const char* in1;
+  int c0, c1, ld0, ld1;
+  int n, h, w, up2;
+  const char* weight; int wld;
+  const float* bias;
+  int cout, kh, kw, stride, pad_t, pad_l, ho, wo;
+  const float* gn_ab; int gn_silu;
+  const float* emb; int emb_ld;
+  int act; float act_param;
+  const char* res; int res_ld;
+  char* out; int out_ld, out_mode;
+  int out_f32;
+  int M, cin, ktot, nk;
+  long in_bs, w_bs, out_bs;  // batched-GEMM strides (elements), blockIdx.z
+  int batch;
+};
+
+constexpr int ROWB = 144;  // LDS bytes per tile row: 128 B of k-data + 16 B pad (bank spread)
+
+template <typename T> struct MmaTraits;
+template <> struct MmaTraits<bf16> {
+  static constexpr int BK = 64;   // k per tile (128 B per row)
+  static constexpr int EPC = 8;   // elements per 16-byte chunk
+};
+template <> struct MmaTraits<float> {
+  static constexpr int BK = 32;
+  static constexpr int EPC = 4;
+};
+
+__device__ __forceinline__ float apply_act(float v, int act, float p) {
+  if (act == 1) return v >= 0.f ? v : v * p;
+  if (act == 2) return gelu_f(v);
+  if (act == 3) return silu_f(v);
+  return v;
+}
+
+// Load 16 bytes (one chunk) from global, or zeros.
+__device__ __forceinline__ uint4 ld16(const char* p) { return *reinterpret_cast<const uint4*>(p); }
+
+template <typename T>
+__device__ __forceinline__ uint4 gn_apply_chunk(uint4 raw, const float* ab, int silu) {
+  constexpr int E = MmaTraits<T>::EPC;
+  T v[E];
+  *reinterpret_cast<uint4*>(v) = raw;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float x = to_f32(v[e]);
+    x = x * ab[2 * e] + ab[2 * e + 1];
+    if (silu) x = silu_f(x);
+    v[e] = from_f32<T>(x);
+  }
+  return *reinterpret_cast<uint4*>(v);
+}
+
+template <typename T, int BM, int BN, int WGM, int WGN, bool VEC>
+__global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
+  constexpr int BK = MmaTraits<T>::BK;
+  constexpr int EPC = MmaTraits<T>::EPC;
+  constexpr int ES = sizeof(T);
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int AR = BM / 32;                  // A chunks per thread (8 chunks per row, 256 threads)
+  constexpr int BR = (BN * 8 + 255) / 256;     // B chunks per thread
+  static_assert(TM >= 1 && TN >= 1, "tile");
+
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  // buffer b: A tile at lds + b*(BM+BN)*ROWB, B tile right after it
+#define AS(b) (lds + (b) * (BM + BN) * ROWB)
+#define BS(b) (lds + (b) * (BM + BN) * ROWB + BM * ROWB)
+
+  if (gridDim.z > 1) {
+    const long z = blockIdx.z;
+    a.in0 += z * a.in_bs * ES; a.in1 += z * a.in_bs * ES;
+    a.weight += z * a.w_bs * ES;
+    a.out += z * a.out_bs * (((sizeof(T) == 4) || a.out_f32) ? 4 : ES);
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kc = tid & 7;   // chunk column this thread gathers (same every k-tile)
+  const int hw_o = a.ho * a.wo;
+  const int hin = a.up2 ? 2 * a.h : a.h, win = a.up2 ? 2 * a.w : a.w;
+
+  // per-row gather state (rows fixed across the K loop)
+  int r_img[AR], r_iy[AR], r_ix[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    int m = m0 + (tid >> 3) + 32 * i;
+    if (m < a.M) {
+      int img = m / hw_o, rem = m - img * hw_o;
+      int oy = rem / a.wo, ox = rem - oy * a.wo;
+      r_img[i] = img;
+      r_iy[i] = oy * a.stride - a.pad_t;
+      r_ix[i] = ox * a.stride - a.pad_l;
+    } else {
+      r_img[i] = -1; r_iy[i] = 0; r_ix[i] = 0;
+    }
+  }
+
+  uint4 areg[AR];
+  uint4 breg[BR];
+  int a_c[AR];  // channel of chunk start per row (for the GN prologue), -1 = zero chunk
+
+  auto gather_a = [&](int kt) {
+    const int k0 = kt * BK + kc * EPC;
+    if constexpr (VEC) {
+      bool kval = k0 < a.ktot;
+      int tap = kval ? k0 / a.cin : 0;
+      int c = k0 - tap * a.cin;
+      int ky = tap / a.kw, kx = tap - ky * a.kw;
+      const char* base; int ld, cs;
+      if (c < a.c0) { base = a.in0; ld = a.ld0; cs = c; } else { base = a.in1; ld = a.ld1; cs = c - a.c0; }
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        int iy = r_iy[i] + ky, ix = r_ix[i] + kx;
+        bool ok = kval && r_img[i] >= 0 && iy >= 0 && iy < hin && ix >= 0 && ix < win;
+        if (ok) {
+          if (a.up2) { iy >>= 1; ix >>= 1; }
+          long pix = ((long)r_img[i] * a.h + iy) * a.w + ix;
+          areg[i] = ld16(base + (pix * ld + cs) * ES);
+          a_c[i] = c;
+        } else {
+          areg[i] = make_uint4(0, 0, 0, 0);
+          a_c[i] = -1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        T v[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          int k = k0 + e;
+          float x = 0.f;
+          if (k < a.ktot && r_img[i] >= 0) {
+            int tap = k / a.cin, c = k - tap * a.cin;
+            int ky = tap / a.kw, kx = tap - ky * a.kw;
+            int iy = r_iy[i] + ky, ix = r_ix[i] + kx;
+            if (iy >= 0 && iy < hin && ix >= 0 && ix < win) {
+              if (a.up2) { iy >>= 1; ix >>= 1; }
+              long pix = ((long)r_img[i] * a.h + iy) * a.w + ix;
+              const T* src = (c < a.c0) ? reinterpret_cast<const T*>(a.in0) + pix * a.ld0 + c
+                                        : reinterpret_cast<const T*>(a.in1) + pix * a.ld1 + (c - a.c0);
+              x = to_f32(*src);
+              if (a.gn_ab) {
+                const float* ab = a.gn_ab + ((long)r_img[i] * a.cin + c) * 2;
+                x = x * ab[0] + ab[1];
+                if (a.gn_silu) x = silu_f(x);
+              }
+            }
+          }
+          v[e] = from_f32<T>(x);
+        }
+        areg[i] = *reinterpret_cast<uint4*>(v);
+        a_c[i] = -1;  // prologue already applied
+      }
+    }
+  };
+
+  auto gather_b = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      int cid = tid + 256 * i;
+      int row = cid >> 3, ch = cid & 7;
+      if (row < BN) {
+        int nn = n0 + row;
+        if (nn < a.cout)
+          breg[i] = ld16(a.weight + ((long)nn * a.wld + kt * BK + ch * EPC) * ES);
+        else
+          breg[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      uint4 v = areg[i];
+      if constexpr (VEC) {
+        if (a.gn_ab && a_c[i] >= 0)
+          v = gn_apply_chunk<T>(v, a.gn_ab + ((long)r_img[i] * a.cin + a_c[i]) * 2, a.gn_silu);
+      }
+      int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(AS(buf) + row * ROWB + kc * 16) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      int cid = tid + 256 * i;
+      int row = cid >> 3, ch = cid & 7;
+      if (row < BN) *reinterpret_cast<uint4*>(BS(buf) + row * ROWB + ch * 16) = breg[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lrow = lane & 15, lq = lane >> 4;
+
+  gather_a(0);
+  gather_b(0);
+  store_tiles(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < a.nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < a.nk) { gather_a(kt + 1); gather_b(kt + 1); }
+    const char* Ab = AS(cur) + (wm * WTM + lrow) * ROWB;
+    const char* Bb = BS(cur) + (wn * WTN + lrow) * ROWB;
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[TM], bfv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROWB + s * 64 + lq * 16);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROWB + s * 64 + lq * 16);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        float af[TM], bfv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const float*>(Ab + i * 16 * ROWB + (s * 4 + lq) * 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const float*>(Bb + j * 16 * ROWB + (s * 4 + lq) * 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < a.nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+#undef AS
+#undef BS
+  // ---------------- epilogue: C[m][n], lane holds col n = lane&15, rows 4*lq + r
+  const bool of32 = (sizeof(T) == 4) || a.out_f32;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
+      if (m >= a.M) continue;
+      const int img = m / hw_o;
+      long opix = m;
+      int oy = 0, ox = 0;
+      if (a.out_mode == 1) { int rem = m - img * hw_o; oy = rem / a.wo; ox = rem - oy * a.wo; }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nn = n0 + wn * WTN + j * 16 + lrow;
+        if (nn >= a.cout) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v += a.bias[nn];
+        if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
+        v = apply_act(v, a.act, a.act_param);
+        long oidx;
+        if (a.out_mode == 1) {
+          int c = nn >> 2, dy = (nn >> 1) & 1, dx = nn & 1;
+          long p = ((long)img * (2 * a.ho) + (2 * oy + dy)) * (2 * a.wo) + (2 * ox + dx);
+          oidx = p * a.out_ld + c;
+          if (a.res) {
+            long ridx = p * a.res_ld + c;
+            v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const T*>(a.res)[ridx]);
+          }
+        } else {
+          oidx = opix * a.out_ld + nn;
+          if (a.res) {
+            long ridx = opix * a.res_ld + nn;
+            v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const T*>(a.res)[ridx]);
+          }
+        }
+        if (of32) reinterpret_cast<float*>(a.out)[oidx] = v;
+        else reinterpret_cast<T*>(a.out)[oidx] = from_f32<T>(v);
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int WGM, int WGN>
+int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
+  dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
+  size_t lds = 2 * (BM + BN) * ROWB;
+  if (vec)
+    hipLaunchKernelGGL((conv_kernel<T, BM, BN, WGM, WGN, true>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((conv_kernel<T, BM, BN, WGM, WGN, false>), grid, dim3(256), lds, s, a);
+  return launch_status();
+}
+
+}  // namespace
+
+extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
+  if (!d || !d->in0 || !d->weight || !d->out) return RDEIC_EINVAL;
+  if (d->c0 <= 0 || d->c1 < 0 || (d->c1 > 0 && !d->in1) || d->cout <= 0 || d->kh <= 0 || d->kw <= 0 ||
+      d->stride <= 0 || d->n <= 0 || d->ho <= 0 || d->wo <= 0)
+    return RDEIC_EINVAL;
+  if (d->dtype != 0 && d->dtype != 1) return RDEIC_EINVAL;
+  ConvArgs a;
+  a.in0 = (const char*)d->in0; a.in1 = (const char*)(d->in1 ? d->in1 : d->in0);
+  a.c0 = d->c0; a.c1 = d->c1; a.ld0 = d->ld0; a.ld1 = d->c1 ? d->ld1 : d->ld0;
+  a.n = d->n; a.h = d->h; a.w = d->w; a.up2 = d->up2;
+  a.weight = (const char*)d->weight; a.wld = d->wld; a.bias = d->bias;
+  a.cout = d->cout; a.kh = d->kh; a.kw = d->kw; a.stride = d->stride; a.pad_t = d->pad_t; a.pad_l = d->pad_l;
+  a.ho = d->ho; a.wo = d->wo;
+  a.gn_ab = d->gn_ab; a.gn_silu = d->gn_silu;
+  a.emb = d->emb; a.emb_ld = d->emb_ld;
+  a.act = d->act; a.act_param = d->act_param;
+  a.res = (const char*)d->res; a.res_ld = d->res_ld;
+  a.out = (char*)d->out; a.out_ld = d->out_ld; a.out_mode = d->out_mode;
+  a.out_f32 = d->out_f32;
+  a.M = d->n * d->ho * d->wo;
+  a.batch = d->batch > 1 ? d->batch : 1;
+  a.in_bs = d->in_bs; a.w_bs = d->w_bs; a.out_bs = d->out_bs;
+  if (a.batch > 1 && (d->res || d->emb || d->out_mode)) return RDEIC_EINVAL;
+  a.cin = d->c0 + d->c1;
+  a.ktot = d->kh * d->kw * a.cin;
+  const int BK = d->dtype == 1 ? 64 : 32;
+  if (d->wld < a.ktot || d->wld % 64 != 0) return RDEIC_EINVAL;
+  a.nk = (a.ktot + BK - 1) / BK;
+  if (d->out_mode == 1 && (d->cout % 4 != 0)) return RDEIC_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int epc = d->dtype == 1 ? 8 : 4;
+  bool vec = (d->c0 % epc == 0) && (d->ld0 % epc == 0) && (((uintptr_t)d->in0) % 16 == 0);
+  if (d->c1) vec = vec && (d->c1 % epc == 0) && (d->ld1 % epc == 0) && (((uintptr_t)d->in1) % 16 == 0);
+  if (((uintptr_t)d->weight) % 16 != 0) return RDEIC_EINVAL;
+
+  if (d->dtype == 1) {
+    if (d->cout <= 16) return launch_cfg<bf16, 128, 16, 4, 1>(a, vec, s);
+    if (d->cout <= 32) return launch_cfg<bf16, 128, 32, 4, 1>(a, vec, s);
+    if (d->cout % 128 != 0 && d->cout % 64 == 0) return launch_cfg<bf16, 128, 64, 2, 2>(a, vec, s);
+    if (a.M <= 4096) return launch_cfg<bf16, 64, 128, 2, 2>(a, vec, s);
+    return launch_cfg<bf16, 128, 128, 2, 2>(a, vec, s);
+  } else {
+    if (d->cout <= 16) return launch_cfg<float, 64, 16, 4, 1>(a, vec, s);
+    return launch_cfg<float, 64, 64, 2, 2>(a, vec, s);
+  }
+}

@@ -1,0 +1,294 @@
+// Elementwise / layout kernels on the RDEIC hot path (gfx950).
+//   * GEGLU gate (attention.py:49-56)
+//   * NCHW fp32 <-> internal NHWC conversions at the API boundary
+//   * q_sample and the relay-DDIM update (ddpm.py:357-360, ddim_sampler_relay.py:203-231)
+//   * sinusoidal timestep embedding (util.py:161-181)
+//   * uint8 image <-> model tensors (inference.py:51-52, 85-87)
+//   * counter-based synthetic weights and weight packing for the implicit-GEMM conv
+#include "common.h"
+#include "../../include/rdeic_hip.h"
+
+// parity-sensitive scalar arithmetic: no fma contraction (matches the reference's separate roundings)
+#pragma clang fp contract(off)
+
+namespace {
+
+template <typename T>
+__global__ void geglu_kernel(const T* __restrict__ in, long rows, int c, int ldin, T* __restrict__ out, int ldout) {
+  long total = rows * c;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long r = i / c;
+    int j = (int)(i - r * c);
+    float x = to_f32(in[r * ldin + j]);
+    float g = to_f32(in[r * ldin + c + j]);
+    out[r * ldout + j] = from_f32<T>(x * gelu_f(g));
+  }
+}
+
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, int n, int c, int hw, float mul, float add,
+                                    T* __restrict__ out, int ld) {
+  long total = (long)n * c * hw;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long img = i / ((long)c * hw);
+    long rem = i - img * c * hw;
+    int ch = (int)(rem / hw);
+    int p = (int)(rem - (long)ch * hw);
+    float v = __fadd_rn(__fmul_rn(in[i], mul), add);
+    out[(img * hw + p) * ld + ch] = from_f32<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(const T* __restrict__ in, int n, int c, int hw, int ld, float mul, float add,
+                                    float* __restrict__ out) {
+  long total = (long)n * c * hw;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long img = i / ((long)c * hw);
+    long rem = i - img * c * hw;
+    int ch = (int)(rem / hw);
+    int p = (int)(rem - (long)ch * hw);
+    out[i] = __fadd_rn(__fmul_rn(to_f32(in[(img * hw + p) * ld + ch]), mul), add);
+  }
+}
+
+// y = a[img] * x + b[img] * z   (q_sample: sqrt(abar_t) * x0 + sqrt(1-abar_t) * noise)
+__global__ void axpby_kernel(const float* __restrict__ x, const float* __restrict__ z, int n_img, int per_img,
+                             const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y) {
+  long total = (long)n_img * per_img;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int img = (int)(i / per_img);
+    y[i] = __fadd_rn(__fmul_rn(a[img], x[i]), __fmul_rn(b[img], z[i]));
+  }
+}
+
+// DDIM (eta = 0) update in the reference's op order:
+//   pred_x0 = (x - sqrt(1-a_t) * e) / sqrt(a_t);   x' = sqrt(a_prev) * pred_x0 + sqrt(1-a_prev-sigma^2) * e
+__global__ void ddim_step_kernel(const float* __restrict__ x, const float* __restrict__ e, long count, float c_sq1m,
+                                 float c_sqa, float c_sqap, float c_dir, float* __restrict__ xp, float* __restrict__ x0) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    float p = __fdiv_rn(__fsub_rn(x[i], __fmul_rn(c_sq1m, e[i])), c_sqa);
+    if (x0) x0[i] = p;
+    xp[i] = __fadd_rn(__fmul_rn(c_sqap, p), __fmul_rn(c_dir, e[i]));
+  }
+}
+
+__global__ void timestep_emb_kernel(const int64_t* __restrict__ t, const float* __restrict__ freqs, int n, int half,
+                                    float* __restrict__ out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * half) return;
+  int r = i / half, j = i - r * half;
+  float arg = __fmul_rn((float)t[r], freqs[j]);
+  out[(long)r * 2 * half + j] = cosf(arg);
+  out[(long)r * 2 * half + half + j] = sinf(arg);
+}
+
+__global__ void silu_f32_kernel(const float* __restrict__ x, float* __restrict__ y, long count) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x)
+    y[i] = x[i] / (1.0f + expf(-x[i]));
+}
+
+// img u8 [n][h][w][3] -> x = (u8/255.0 (fp64, then fp32)) * 2 - 1 written NHWC (ld >= 3)
+template <typename T>
+__global__ void img_to_nhwc_kernel(const uint8_t* __restrict__ img, long pix, T* __restrict__ out, int ld) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pix * 3; i += (long)gridDim.x * blockDim.x) {
+    long p = i / 3;
+    int ch = (int)(i - p * 3);
+    float v = (float)((double)img[i] / 255.0);
+    v = __fsub_rn(__fmul_rn(v, 2.0f), 1.0f);
+    out[p * ld + ch] = from_f32<T>(v);
+  }
+}
+
+// x (decoded, ~[-1,1]) -> ((x+1)/2).clamp(0,1) * 255 truncated to uint8
+template <typename T>
+__global__ void nhwc_to_img_kernel(const T* __restrict__ x, long pix, int ld, uint8_t* __restrict__ img) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pix * 3; i += (long)gridDim.x * blockDim.x) {
+    long p = i / 3;
+    int ch = (int)(i - p * 3);
+    float v = __fdiv_rn(__fadd_rn(to_f32(x[p * ld + ch]), 1.0f), 2.0f);
+    v = fminf(fmaxf(v, 0.0f), 1.0f);
+    v = __fmul_rn(v, 255.0f);
+    v = fminf(fmaxf(v, 0.0f), 255.0f);
+    img[i] = (uint8_t)(int)v;
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  uint64_t z = x;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void fill_uniform_kernel(float* __restrict__ out, long count, uint64_t seed, float scale, float offset) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    uint64_t r = splitmix64(seed + (uint64_t)i);
+    float u = (float)((int)(r >> 40) - 8388608);  // exact integer in [-2^23, 2^23)
+    out[i] = __fadd_rn(__fmul_rn(u, scale), offset);
+  }
+}
+
+// torch conv weight [cout][cin][kh][kw] -> packed [cout][wld], k = (ky*kw + kx)*cin + ci, zero tail
+template <typename T>
+__global__ void pack_conv_kernel(const float* __restrict__ w, int cout, int cin, int kh, int kw, T* __restrict__ out,
+                                 int wld) {
+  long total = (long)cout * wld;
+  int ktot = kh * kw * cin;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int co = (int)(i / wld);
+    int k = (int)(i - (long)co * wld);
+    float v = 0.f;
+    if (k < ktot) {
+      int tap = k / cin, ci = k - tap * cin;
+      int ky = tap / kw, kx = tap - ky * kw;
+      v = w[(((long)co * cin + ci) * kh + ky) * kw + kx];
+    }
+    out[i] = from_f32<T>(v);
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ in, TO* __restrict__ out, long count) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x)
+    out[i] = from_f32<TO>(to_f32(in[i]));
+}
+
+inline int grid_for(long total) { return (int)std::max<long>(1, std::min<long>((total + 255) / 256, 16384)); }
+
+}  // namespace
+
+extern "C" int rdeic_geglu(const void* in, int32_t rows, int32_t c, int32_t ldin, void* out, int32_t ldout,
+                           int32_t dtype, void* stream) {
+  if (!in || !out || rows <= 0 || c <= 0) return RDEIC_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int g = grid_for((long)rows * c);
+  if (dtype == 1)
+    hipLaunchKernelGGL(geglu_kernel<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)in, (long)rows, c, ldin, (bf16*)out,
+                       ldout);
+  else
+    hipLaunchKernelGGL(geglu_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, (long)rows, c, ldin,
+                       (float*)out, ldout);
+  return launch_status();
+}
+
+extern "C" int rdeic_nchw_to_nhwc(const float* in, int32_t n, int32_t c, int32_t h, int32_t w, float mul, float add,
+                                  void* out, int32_t ld, int32_t dtype, void* stream) {
+  if (!in || !out || n <= 0 || c <= 0 || ld < c) return RDEIC_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int g = grid_for((long)n * c * h * w);
+  if (dtype == 1)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(g), dim3(256), 0, s, in, n, c, h * w, mul, add, (bf16*)out, ld);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(g), dim3(256), 0, s, in, n, c, h * w, mul, add, (float*)out,
+                       ld);
+  return launch_status();
+}
+
+extern "C" int rdeic_nhwc_to_nchw(const void* in, int32_t n, int32_t c, int32_t h, int32_t w, int32_t ld, float mul,
+                                  float add, float* out, int32_t dtype, void* stream) {
+  if (!in || !out || n <= 0 || c <= 0 || ld < c) return RDEIC_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int g = grid_for((long)n * c * h * w);
+  if (dtype == 1)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)in, n, c, h * w, ld, mul, add,
+                       out);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)in, n, c, h * w, ld, mul,
+                       add, out);
+  return launch_status();
+}
+
+extern "C" int rdeic_axpby(const float* x, const float* z, int32_t n_img, int32_t per_img, const float* a,
+                           const float* b, float* y, void* stream) {
+  if (!x || !z || !a || !b || !y || n_img <= 0 || per_img <= 0) return RDEIC_EINVAL;
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for((long)n_img * per_img)), dim3(256), 0, (hipStream_t)stream, x, z,
+                     n_img, per_img, a, b, y);
+  return launch_status();
+}
+
+extern "C" int rdeic_ddim_step(const float* x, const float* e, int64_t count, float c_sq1m, float c_sqa, float c_sqap,
+                               float c_dir, float* xp, float* x0, void* stream) {
+  if (!x || !e || !xp || count <= 0) return RDEIC_EINVAL;
+  hipLaunchKernelGGL(ddim_step_kernel, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream, x, e, (long)count,
+                     c_sq1m, c_sqa, c_sqap, c_dir, xp, x0);
+  return launch_status();
+}
+
+extern "C" int rdeic_timestep_embedding(const int64_t* t, const float* freqs, int32_t n, int32_t dim, float* out,
+                                        void* stream) {
+  if (!t || !freqs || !out || n <= 0 || dim <= 0 || (dim & 1)) return RDEIC_EINVAL;
+  int half = dim / 2;
+  hipLaunchKernelGGL(timestep_emb_kernel, dim3((n * half + 255) / 256), dim3(256), 0, (hipStream_t)stream, t, freqs, n,
+                     half, out);
+  return launch_status();
+}
+
+extern "C" int rdeic_silu_f32(const float* x, float* y, int64_t count, void* stream) {
+  if (!x || !y || count <= 0) return RDEIC_EINVAL;
+  hipLaunchKernelGGL(silu_f32_kernel, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream, x, y, (long)count);
+  return launch_status();
+}
+
+extern "C" int rdeic_image_u8_to_nhwc(const uint8_t* img, int32_t n, int32_t h, int32_t w, void* out, int32_t ld,
+                                      int32_t dtype, void* stream) {
+  if (!img || !out || n <= 0 || h <= 0 || w <= 0 || ld < 3) return RDEIC_EINVAL;
+  long pix = (long)n * h * w;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1)
+    hipLaunchKernelGGL(img_to_nhwc_kernel<bf16>, dim3(grid_for(pix * 3)), dim3(256), 0, s, img, pix, (bf16*)out, ld);
+  else
+    hipLaunchKernelGGL(img_to_nhwc_kernel<float>, dim3(grid_for(pix * 3)), dim3(256), 0, s, img, pix, (float*)out, ld);
+  return launch_status();
+}
+
+extern "C" int rdeic_nhwc_to_image_u8(const void* x, int32_t n, int32_t h, int32_t w, int32_t ld, uint8_t* img,
+                                      int32_t dtype, void* stream) {
+  if (!x || !img || n <= 0 || h <= 0 || w <= 0 || ld < 3) return RDEIC_EINVAL;
+  long pix = (long)n * h * w;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1)
+    hipLaunchKernelGGL(nhwc_to_img_kernel<bf16>, dim3(grid_for(pix * 3)), dim3(256), 0, s, (const bf16*)x, pix, ld, img);
+  else
+    hipLaunchKernelGGL(nhwc_to_img_kernel<float>, dim3(grid_for(pix * 3)), dim3(256), 0, s, (const float*)x, pix, ld,
+                       img);
+  return launch_status();
+}
+
+extern "C" int rdeic_fill_uniform(float* out, int64_t count, uint64_t seed, float scale, float offset, void* stream) {
+  if (!out || count < 0) return RDEIC_EINVAL;
+  if (count == 0) return RDEIC_OK;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream, out, (long)count,
+                     seed, scale, offset);
+  return launch_status();
+}
+
+extern "C" int rdeic_pack_conv_weight(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out,
+                                      int32_t wld, int32_t dtype, void* stream) {
+  if (!w || !out || cout <= 0 || cin <= 0 || wld < kh * kw * cin) return RDEIC_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int g = grid_for((long)cout * wld);
+  if (dtype == 1)
+    hipLaunchKernelGGL(pack_conv_kernel<bf16>, dim3(g), dim3(256), 0, s, w, cout, cin, kh, kw, (bf16*)out, wld);
+  else
+    hipLaunchKernelGGL(pack_conv_kernel<float>, dim3(g), dim3(256), 0, s, w, cout, cin, kh, kw, (float*)out, wld);
+  return launch_status();
+}
+
+extern "C" int rdeic_cast(const void* in, int32_t in_dtype, void* out, int32_t out_dtype, int64_t count, void* stream) {
+  if (!in || !out || count < 0) return RDEIC_EINVAL;
+  if (count == 0) return RDEIC_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int g = grid_for(count);
+  if (in_dtype == 0 && out_dtype == 1)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(g), dim3(256), 0, s, (const float*)in, (bf16*)out, (long)count);
+  else if (in_dtype == 1 && out_dtype == 0)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(g), dim3(256), 0, s, (const bf16*)in, (float*)out, (long)count);
+  else if (in_dtype == 0 && out_dtype == 0)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, (const float*)in, (float*)out,
+                       (long)count);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(g), dim3(256), 0, s, (const bf16*)in, (bf16*)out, (long)count);
+  return launch_status();
+}

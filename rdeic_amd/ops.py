@@ -1,0 +1,295 @@
+"""Tensor-level wrappers over the C ABI (device buffers are torch tensors; torch is plumbing).
+
+Activation convention: NHWC tensors of shape [n, h, w, c] whose channel dim is contiguous
+(stride(3) == 1) and whose pixels are evenly strided (stride(2) = ld >= c, stride(1) = w*ld,
+stride(0) = h*w*ld). A channel slice ``x[..., a:b]`` of such a tensor is again valid, which
+is how the reference's torch.cat / channel slicing is expressed without copies.
+Token tensors for linear layers are [rows, c] with stride(1) == 1.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import ConvDesc, call
+
+NONE, LEAKY, GELU, SILU = 0, 1, 2, 3
+
+
+def dt_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError(f"unsupported activation dtype {t.dtype}")
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def pix_ld(x: torch.Tensor) -> int:
+    """Pixel stride of an NHWC activation (validates the layout)."""
+    if x.dim() != 4 or x.stride(3) != 1:
+        raise ValueError(f"expected NHWC activation with contiguous channels, got shape {tuple(x.shape)} "
+                         f"strides {x.stride()}")
+    n, h, w, c = x.shape
+    ld = x.stride(2)
+    if ld < c or (h > 1 and x.stride(1) != w * ld) or (n > 1 and x.stride(0) != h * w * ld):
+        raise ValueError(f"activation pixels not evenly strided: shape {tuple(x.shape)} strides {x.stride()}")
+    return ld
+
+
+def new_act(n: int, h: int, w: int, c: int, dtype, device=None) -> torch.Tensor:
+    return torch.empty((n, h, w, c), dtype=dtype, device=device or "cuda")
+
+
+@dataclass
+class ConvParams:
+    """A conv / linear layer packed for rdeic_conv2d: weight [cout][wld] (K = (ky, kx, ci))."""
+    weight: torch.Tensor
+    wld: int
+    bias: Optional[torch.Tensor]
+    cout: int
+    cin: int
+    kh: int
+    kw: int
+    stride: int = 1
+    pad: int = 0
+
+    @staticmethod
+    def pack(w: torch.Tensor, b: Optional[torch.Tensor], stride: int = 1, pad: int = 0,
+             dtype=torch.bfloat16) -> "ConvParams":
+        """Pack an fp32 torch-layout weight ([cout, cin, kh, kw] or Linear [cout, cin]) on device."""
+        if w.dim() == 2:
+            w = w[:, :, None, None]
+        w = w.detach().to(device="cuda", dtype=torch.float32).contiguous()
+        cout, cin, kh, kw = w.shape
+        wld = ((kh * kw * cin + 63) // 64) * 64
+        packed = torch.empty((cout, wld), dtype=dtype, device="cuda")
+        call("rdeic_pack_conv_weight", w.data_ptr(), cout, cin, kh, kw, packed.data_ptr(), wld,
+             1 if dtype == torch.bfloat16 else 0, stream_ptr())
+        bias = None if b is None else b.detach().to(device="cuda", dtype=torch.float32).contiguous()
+        return ConvParams(packed, wld, bias, cout, cin, kh, kw, stride, pad)
+
+
+def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None, up2: bool = False,
+           pad_t: Optional[int] = None, pad_l: Optional[int] = None, out_hw=None,
+           gn: Optional[torch.Tensor] = None, gn_silu: bool = False, emb: Optional[torch.Tensor] = None,
+           act: int = NONE, slope: float = 0.0, res: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False) -> torch.Tensor:
+    """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC)."""
+    n, h, w, c0 = x.shape
+    ld0 = pix_ld(x)
+    c1, ld1 = 0, 0
+    if x2 is not None:
+        if x2.shape[:3] != x.shape[:3] or x2.dtype != x.dtype:
+            raise ValueError("concat inputs must share n, h, w and dtype")
+        c1 = x2.shape[3]
+        ld1 = pix_ld(x2)
+    if c0 + c1 != p.cin:
+        raise ValueError(f"conv expects cin={p.cin}, got {c0}+{c1}")
+    if p.weight.dtype != x.dtype:
+        raise TypeError(f"weight dtype {p.weight.dtype} != activation dtype {x.dtype}")
+    hi, wi = (2 * h, 2 * w) if up2 else (h, w)
+    pt = p.pad if pad_t is None else pad_t
+    pl = p.pad if pad_l is None else pad_l
+    if out_hw is None:
+        ho = (hi + 2 * p.pad - p.kh) // p.stride + 1
+        wo = (wi + 2 * p.pad - p.kw) // p.stride + 1
+    else:
+        ho, wo = out_hw
+    odt = torch.float32 if (out_f32 or x.dtype == torch.float32) else x.dtype
+    if pixel_shuffle:
+        oshape = (n, 2 * ho, 2 * wo, p.cout // 4)
+    else:
+        oshape = (n, ho, wo, p.cout)
+    if out is None:
+        out = torch.empty(oshape, dtype=odt, device=x.device)
+    elif tuple(out.shape) != oshape or out.dtype != odt:
+        raise ValueError(f"out has shape {tuple(out.shape)}/{out.dtype}, expected {oshape}/{odt}")
+    d = ConvDesc()
+    d.in0 = x.data_ptr()
+    d.in1 = _ptr(x2)
+    d.c0, d.c1, d.ld0, d.ld1 = c0, c1, ld0, ld1
+    d.n, d.h, d.w, d.up2 = n, h, w, int(up2)
+    d.weight, d.wld, d.bias = p.weight.data_ptr(), p.wld, _ptr(p.bias)
+    d.cout, d.kh, d.kw, d.stride, d.pad_t, d.pad_l = p.cout, p.kh, p.kw, p.stride, pt, pl
+    d.ho, d.wo = ho, wo
+    if gn is not None:
+        if gn.shape != (n, p.cin, 2):
+            raise ValueError("gn affine must be [n, cin, 2]")
+        d.gn_ab = gn.data_ptr()
+        d.gn_silu = int(gn_silu)
+    if emb is not None:
+        if emb.dtype != torch.float32 or emb.shape[0] != n or emb.stride(1) != 1:
+            raise ValueError("emb must be fp32 [n, >=cout] row-major")
+        d.emb = emb.data_ptr()
+        d.emb_ld = emb.stride(0)
+    d.act, d.act_param = act, float(slope)
+    if res is not None:
+        if tuple(res.shape) != oshape or res.dtype != odt:
+            raise ValueError(f"residual {tuple(res.shape)}/{res.dtype} does not match output {oshape}/{odt}")
+        d.res = res.data_ptr()
+        d.res_ld = pix_ld(res)
+    d.out = out.data_ptr()
+    d.out_ld = pix_ld(out)
+    d.out_mode = 1 if pixel_shuffle else 0
+    d.dtype = dt_code(x)
+    d.out_f32 = int(odt == torch.float32 and x.dtype != torch.float32)
+    d.batch = 1
+    call("rdeic_conv2d", C.byref(d), stream_ptr())
+    return out
+
+
+def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, out_f32: bool = False) -> torch.Tensor:
+    """Token-wise Linear over a [rows, c] tensor (1x1 conv over a rows x 1 image)."""
+    rows, c = x.shape
+    x4 = x.as_strided((1, rows, 1, c), (rows * x.stride(0), x.stride(0), x.stride(0), 1))
+    odt = torch.float32 if (out_f32 or x.dtype == torch.float32) else x.dtype
+    if out is None:
+        out = torch.empty((rows, p.cout), dtype=odt, device=x.device)
+    o4 = out.as_strided((1, rows, 1, p.cout), (rows * out.stride(0), out.stride(0), out.stride(0), 1))
+    r4 = None
+    if res is not None:
+        r4 = res.as_strided((1, rows, 1, p.cout), (rows * res.stride(0), res.stride(0), res.stride(0), 1))
+    conv2d(x4, p, act=act, res=r4, out=o4, out_f32=out_f32)
+    return out
+
+
+def gemm_batched(a: torch.Tensor, b_nk: torch.Tensor, out: torch.Tensor, *, batch: int, m: int, n: int, k: int,
+                 lda: int, ldb: int, a_bs: int, b_bs: int, out_bs: int) -> torch.Tensor:
+    """out[z] (m x n, row stride n) = A[z] (m x k, row stride lda) . B[z]^T (B stored n x k, row stride ldb).
+    ldb must be a multiple of 64 and B zero beyond k (it is used as a packed weight)."""
+    d = ConvDesc()
+    d.in0 = a.data_ptr()
+    d.c0, d.ld0 = k, lda
+    d.n, d.h, d.w = 1, m, 1
+    d.weight, d.wld = b_nk.data_ptr(), ldb
+    d.cout, d.kh, d.kw, d.stride = n, 1, 1, 1
+    d.ho, d.wo = m, 1
+    d.out = out.data_ptr()
+    d.out_ld = n
+    d.dtype = dt_code(a)
+    d.out_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
+    d.batch = batch
+    d.in_bs, d.w_bs, d.out_bs = a_bs, b_bs, out_bs
+    call("rdeic_conv2d", C.byref(d), stream_ptr())
+    return out
+
+
+def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float) -> torch.Tensor:
+    """Per-(image, channel) affine [n, c, 2] such that GroupNorm(x) = x*a + b."""
+    n, h, w, c = x.shape
+    ld = pix_ld(x)
+    ws = torch.empty(int(_lib.load().rdeic_groupnorm_ws_floats(n, h * w, c)), dtype=torch.float32, device=x.device)
+    ab = torch.empty((n, c, 2), dtype=torch.float32, device=x.device)
+    call("rdeic_groupnorm_stats", x.data_ptr(), n, h * w, c, ld, groups, float(eps), gamma.data_ptr(),
+         beta.data_ptr(), ab.data_ptr(), ws.data_ptr(), dt_code(x), stream_ptr())
+    return ab
+
+
+def group_norm_apply(x: torch.Tensor, ab: torch.Tensor, silu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)
+    call("rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(), int(silu), out.data_ptr(),
+         pix_ld(out), dt_code(x), stream_ptr())
+    return out
+
+
+def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    rows, c = x.shape
+    if out is None:
+        out = torch.empty((rows, c), dtype=x.dtype, device=x.device)
+    call("rdeic_layernorm", x.data_ptr(), rows, c, x.stride(0), gamma.data_ptr(), beta.data_ptr(), float(eps),
+         out.data_ptr(), out.stride(0), dt_code(x), stream_ptr())
+    return out
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, *, batch: int, heads: int,
+              lq: int, lk: int, dh: int, scale: float) -> torch.Tensor:
+    """Flash attention over [batch*lq, heads*dh]-layout projections (row strides from the tensors)."""
+    call("rdeic_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
+         out.data_ptr(), out.stride(0), batch, heads, lq, lk, dh, float(scale), dt_code(q), stream_ptr())
+    return out
+
+
+def attention_single_head_materialized(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, *,
+                                       batch: int, length: int, dim: int, scale: float) -> torch.Tensor:
+    """softmax(q k^T * scale) v for one head with a large head dim (VAE AttnBlock, d=512):
+    S = Q K^T (batched MFMA GEMM, fp32) -> row softmax -> O = P V (batched GEMM)."""
+    if dim % 64 != 0 or length % 64 != 0:
+        raise ValueError("materialised attention needs dim, length multiples of 64")
+    dt = dt_code(q)
+    s = torch.empty((batch, length, length), dtype=torch.float32, device=q.device)
+    gemm_batched(q, k, s, batch=batch, m=length, n=length, k=dim, lda=q.stride(0), ldb=k.stride(0),
+                 a_bs=length * q.stride(0), b_bs=length * k.stride(0), out_bs=length * length)
+    p = torch.empty((batch, length, length), dtype=q.dtype, device=q.device)
+    call("rdeic_softmax_rows", s.data_ptr(), batch * length, length, float(scale), p.data_ptr(), dt, stream_ptr())
+    del s
+    vt = torch.empty((batch, dim, length), dtype=q.dtype, device=q.device)
+    call("rdeic_transpose", v.data_ptr(), length, dim, v.stride(0), vt.data_ptr(), length, batch,
+         length * v.stride(0), dim * length, dt, stream_ptr())
+    gemm_batched(p, vt, out, batch=batch, m=length, n=dim, k=length, lda=length, ldb=length,
+                 a_bs=length * length, b_bs=dim * length, out_bs=length * out.stride(0))
+    return out
+
+
+def geglu(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    rows, c2 = x.shape
+    c = c2 // 2
+    if out is None:
+        out = torch.empty((rows, c), dtype=x.dtype, device=x.device)
+    call("rdeic_geglu", x.data_ptr(), rows, c, x.stride(0), out.data_ptr(), out.stride(0), dt_code(x), stream_ptr())
+    return out
+
+
+def nchw_to_nhwc(x: torch.Tensor, dtype, mul: float = 1.0, add: float = 0.0, out=None) -> torch.Tensor:
+    x = x.to(torch.float32).contiguous()
+    n, c, h, w = x.shape
+    if out is None:
+        out = torch.empty((n, h, w, c), dtype=dtype, device=x.device)
+    call("rdeic_nchw_to_nhwc", x.data_ptr(), n, c, h, w, float(mul), float(add), out.data_ptr(), pix_ld(out),
+         dt_code(out), stream_ptr())
+    return out
+
+
+def nhwc_to_nchw(x: torch.Tensor, mul: float = 1.0, add: float = 0.0) -> torch.Tensor:
+    n, h, w, c = x.shape
+    out = torch.empty((n, c, h, w), dtype=torch.float32, device=x.device)
+    call("rdeic_nhwc_to_nchw", x.data_ptr(), n, c, h, w, pix_ld(x), float(mul), float(add), out.data_ptr(),
+         dt_code(x), stream_ptr())
+    return out
+
+
+def cast(x: torch.Tensor, dtype) -> torch.Tensor:
+    x = x.contiguous()
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    call("rdeic_cast", x.data_ptr(), dt_code(x), out.data_ptr(), dt_code(out), x.numel(), stream_ptr())
+    return out
+
+
+def fill_uniform(out: torch.Tensor, seed: int, scale: float, offset: float) -> torch.Tensor:
+    if out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("fill_uniform expects a contiguous fp32 tensor")
+    call("rdeic_fill_uniform", out.data_ptr(), out.numel(), C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+         float(scale) * 2.0 ** -23, float(offset), stream_ptr())
+    return out
+
+
+def silu_f32(x: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(x)
+    call("rdeic_silu_f32", x.data_ptr(), out.data_ptr(), x.numel(), stream_ptr())
+    return out

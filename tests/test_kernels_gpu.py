@@ -1,0 +1,192 @@
+"""Kernel-level numerics on the MI355X: each HIP kernel against a plain PyTorch fp32 (CPU)
+reference of the same op. fp32 parity mode must agree to ~1e-5 relative; bf16 mode to the
+bf16 rounding of its inputs."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _nhwc(x):  # NCHW cpu -> NHWC cuda
+    return x.permute(0, 2, 3, 1).contiguous().cuda()
+
+
+def _nchw(x):
+    return x.float().cpu().permute(0, 3, 1, 2)
+
+
+def _tol(dtype):
+    return (2e-5, 2e-5) if dtype == torch.float32 else (3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,stride,pad,h", [
+    (64, 64, 3, 1, 1, 16), (128, 320, 3, 1, 1, 12), (320, 640, 3, 2, 1, 16), (4, 320, 3, 1, 1, 8),
+    (256, 16, 5, 1, 2, 8), (48, 224, 5, 1, 2, 8), (512, 8, 1, 1, 0, 8), (260, 64, 3, 1, 1, 8),
+    (3, 128, 3, 1, 1, 16), (256, 1024, 1, 1, 0, 4)])
+def test_conv2d(gpu, dtype, cin, cout, k, stride, pad, h):
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(cin * 1000 + cout)
+    x = torch.randn(2, cin, h, h + 2, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / math.sqrt(cin * k * k)
+    b = torch.randn(cout, generator=g)
+    p = ops.ConvParams.pack(w, b, stride=stride, pad=pad, dtype=dtype)
+    xq = x.to(dtype).float()
+    wq = w.to(dtype).float()
+    ref = F.conv2d(xq, wq, b, stride=stride, padding=pad)
+    out = ops.conv2d(_nhwc(x.to(dtype)), p)
+    torch.cuda.synchronize()
+    rt, at = _tol(dtype)
+    torch.testing.assert_close(_nchw(out), ref, rtol=rt, atol=at * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv2d_fusions(gpu, dtype):
+    """concat + GN/SiLU prologue + emb + leaky + residual; up2; asymmetric pad; pixel shuffle."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(7)
+    n, c1, c2, co, h = 2, 64, 32, 64, 8
+    xa = torch.randn(n, c1, h, h, generator=g) * 2 + 1
+    xb = torch.randn(n, c2, h, h, generator=g)
+    w = torch.randn(co, c1 + c2, 3, 3, generator=g) / math.sqrt(9 * (c1 + c2))
+    b = torch.randn(co, generator=g)
+    emb = torch.randn(n, co, generator=g)
+    res = torch.randn(n, co, h, h, generator=g)
+    gamma = torch.rand(c1 + c2, generator=g) + 0.5
+    beta = torch.randn(c1 + c2, generator=g) * 0.1
+    xcat = torch.cat([xa, xb], 1)
+    xq = xcat.to(dtype).float()
+    gn = F.group_norm(xq, 32, gamma, beta, eps=1e-5)
+    ref = F.conv2d(F.silu(gn).to(dtype).float(), w.to(dtype).float(), b, padding=1) + emb[:, :, None, None]
+    ref = F.leaky_relu(ref, 0.1) + res.to(dtype).float()
+    p = ops.ConvParams.pack(w, b, pad=1, dtype=dtype)
+    xa_d, xb_d = _nhwc(xa.to(dtype)), _nhwc(xb.to(dtype))
+    # GN stats over the concatenation: build it explicitly for the stats kernel
+    xcat_d = _nhwc(xcat.to(dtype))
+    ab = ops.group_norm_ab(xcat_d, gamma.cuda(), beta.cuda(), 32, 1e-5)
+    out = ops.conv2d(xa_d, p, x2=xb_d, gn=ab, gn_silu=True, emb=emb.cuda(), act=ops.LEAKY, slope=0.1,
+                     res=_nhwc(res.to(dtype)))
+    torch.cuda.synchronize()
+    rt, at = _tol(dtype)
+    torch.testing.assert_close(_nchw(out), ref, rtol=rt, atol=at * 4)
+
+    # nearest x2 upsample + conv
+    wu = torch.randn(32, c1, 3, 3, generator=g) / math.sqrt(9 * c1)
+    pu = ops.ConvParams.pack(wu, None, pad=1, dtype=dtype)
+    refu = F.conv2d(F.interpolate(xa.to(dtype).float(), scale_factor=2, mode="nearest"), wu.to(dtype).float(),
+                    padding=1)
+    outu = ops.conv2d(xa_d, pu, up2=True)
+    torch.testing.assert_close(_nchw(outu), refu, rtol=rt, atol=at * 4)
+
+    # VAE downsample: pad (0,1,0,1) then stride-2 conv, pad 0
+    pd = ops.ConvParams.pack(wu, None, stride=2, pad=0, dtype=dtype)
+    refd = F.conv2d(F.pad(xa.to(dtype).float(), (0, 1, 0, 1)), wu.to(dtype).float(), stride=2)
+    outd = ops.conv2d(xa_d, pd, pad_t=0, pad_l=0, out_hw=(h // 2, h // 2))
+    torch.testing.assert_close(_nchw(outd), refd, rtol=rt, atol=at * 4)
+
+    # subpel: 1x1 conv to 4C then PixelShuffle(2), leaky 0.01
+    ws = torch.randn(4 * 16, c1, 1, 1, generator=g) / math.sqrt(c1)
+    bs = torch.randn(4 * 16, generator=g)
+    ps = ops.ConvParams.pack(ws, bs, dtype=dtype)
+    refs = F.leaky_relu(F.pixel_shuffle(F.conv2d(xa.to(dtype).float(), ws.to(dtype).float(), bs), 2), 0.01)
+    outs = ops.conv2d(xa_d, ps, pixel_shuffle=True, act=ops.LEAKY, slope=0.01)
+    torch.testing.assert_close(_nchw(outs), refs, rtol=rt, atol=at * 4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c,groups,hw", [(128, 32, 64), (320, 32, 24), (1280, 32, 8), (64, 32, 40)])
+def test_groupnorm(gpu, dtype, c, groups, hw):
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(c + hw)
+    x = torch.randn(2, c, hw, hw + 1, generator=g) * 3 + 5
+    gamma = torch.rand(c, generator=g) + 0.5
+    beta = torch.randn(c, generator=g)
+    xq = x.to(dtype).float()
+    ref = F.silu(F.group_norm(xq, groups, gamma, beta, eps=1e-6))
+    xd = _nhwc(x.to(dtype))
+    ab = ops.group_norm_ab(xd, gamma.cuda(), beta.cuda(), groups, 1e-6)
+    out = ops.group_norm_apply(xd, ab, silu=True)
+    torch.cuda.synchronize()
+    rt, at = (1e-4, 1e-4) if dtype == torch.float32 else (2e-2, 2e-2)
+    torch.testing.assert_close(_nchw(out), ref, rtol=rt, atol=at)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_geglu(gpu, dtype):
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(77, 320, generator=g) * 2 + 1
+    gamma, beta = torch.rand(320, generator=g) + 0.5, torch.randn(320, generator=g)
+    ref = F.layer_norm(x.to(dtype).float(), (320,), gamma, beta, 1e-5)
+    out = ops.layer_norm(x.to(dtype).cuda(), gamma.cuda(), beta.cuda(), 1e-5)
+    rt, at = (1e-5, 1e-5) if dtype == torch.float32 else (2e-2, 2e-2)
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=rt, atol=at)
+    y = torch.randn(50, 2 * 96, generator=g)
+    yq = y.to(dtype).float()
+    refg = yq[:, :96] * F.gelu(yq[:, 96:])
+    outg = ops.geglu(y.to(dtype).cuda())
+    torch.testing.assert_close(outg.float().cpu(), refg, rtol=rt, atol=at)
+
+
+def _ref_attn(q, k, v, heads, dh, scale):
+    b, lq, _ = q.shape
+    lk = k.shape[1]
+    qh = q.view(b, lq, heads, dh).permute(0, 2, 1, 3)
+    kh = k.view(b, lk, heads, dh).permute(0, 2, 1, 3)
+    vh = v.view(b, lk, heads, dh).permute(0, 2, 1, 3)
+    s = torch.einsum("bhid,bhjd->bhij", qh, kh) * scale
+    o = torch.einsum("bhij,bhjd->bhid", s.softmax(-1), vh)
+    return o.permute(0, 2, 1, 3).reshape(b, lq, heads * dh)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("heads,dh,lq,lk", [(5, 64, 256, 256), (4, 16, 300, 300), (10, 64, 64, 77), (16, 16, 64, 77),
+                                           (20, 64, 100, 33)])
+def test_attention(gpu, dtype, heads, dh, lq, lk):
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(heads * dh + lq)
+    b = 2
+    q = torch.randn(b, lq, heads * dh, generator=g)
+    k = torch.randn(b, lk, heads * dh, generator=g)
+    v = torch.randn(b, lk, heads * dh, generator=g)
+    scale = dh ** -0.5
+    ref = _ref_attn(q.to(dtype).float(), k.to(dtype).float(), v.to(dtype).float(), heads, dh, scale)
+    qd = q.to(dtype).cuda().view(b * lq, -1)
+    kd = k.to(dtype).cuda().view(b * lk, -1)
+    vd = v.to(dtype).cuda().view(b * lk, -1)
+    out = torch.empty_like(qd)
+    ops.attention(qd, kd, vd, out, batch=b, heads=heads, lq=lq, lk=lk, dh=dh, scale=scale)
+    torch.cuda.synchronize()
+    rt, at = (2e-5, 2e-5) if dtype == torch.float32 else (3e-2, 3e-2)
+    torch.testing.assert_close(out.float().cpu().view(b, lq, -1), ref, rtol=rt, atol=at)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_attention_materialized(gpu, dtype):
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(11)
+    b, L, d = 2, 256, 512
+    q = torch.randn(b, L, d, generator=g)
+    k = torch.randn(b, L, d, generator=g)
+    v = torch.randn(b, L, d, generator=g)
+    ref = _ref_attn(q.to(dtype).float(), k.to(dtype).float(), v.to(dtype).float(), 1, d, d ** -0.5)
+    qd, kd, vd = (t.to(dtype).cuda().view(b * L, d) for t in (q, k, v))
+    out = torch.empty_like(qd)
+    ops.attention_single_head_materialized(qd, kd, vd, out, batch=b, length=L, dim=d, scale=d ** -0.5)
+    torch.cuda.synchronize()
+    rt, at = (1e-4, 1e-4) if dtype == torch.float32 else (3e-2, 3e-2)
+    torch.testing.assert_close(out.float().cpu().view(b, L, d), ref, rtol=rt, atol=at)
+
+
+def test_fill_uniform_matches_oracle(gpu):
+    """The device weight generator is bit-identical to the CPU oracle generator."""
+    from rdeic_amd import ops
+    from oracle import weights_cpu
+    n = 100003
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    ops.fill_uniform(out, 123456789, 0.05, 1.0)
+    ref = weights_cpu.fill_uniform(n, 123456789, 0.05, 1.0)
+    assert torch.equal(out.cpu(), torch.from_numpy(ref))
