@@ -34,3 +34,6 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle
+
+# parity-sensitive scalar kernels: no fma contraction anywhere in these TUs (headers included)
+$(BUILD)/elementwise.hip.o $(BUILD)/entropy.hip.o: HIPFLAGS += -ffp-contract=off

@@ -80,12 +80,14 @@ int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
  * so that consumers apply y = x*a + b (optionally SiLU) inside their own loads.
  * ws: fp32 workspace of at least rdeic_groupnorm_ws_floats(n, hw, c) floats. */
 size_t rdeic_groupnorm_ws_floats(int32_t n, int32_t hw, int32_t c);
-int rdeic_groupnorm_stats(const void* x, int32_t n, int32_t hw, int32_t c, int32_t ld, int32_t groups,
-                          float eps, const float* gamma, const float* beta, float* ab, float* ws,
-                          int32_t dtype, void* stream);
-/* y = silu?(x*a + b) materialised (NHWC), used where the consumer is not a conv. */
+/* The input is the channel concatenation of x0 [n][hw][ld0] (c0 ch) and, if c1 > 0, x1 (c1 ch). */
+int rdeic_groupnorm_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1, int32_t ld1,
+                          int32_t n, int32_t hw, int32_t groups, float eps, const float* gamma, const float* beta,
+                          float* ab, float* ws, int32_t dtype, void* stream);
+/* y = silu?(x*a + b) * out_mul materialised (NHWC), where the consumer is not a conv
+ * (e.g. the VAE encoder's c = swish(norm_out(h)), followed by the 0.18215 latent scale). */
 int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32_t c, int32_t ld, const float* ab,
-                          int32_t silu, void* y, int32_t yld, int32_t dtype, void* stream);
+                          int32_t silu, float out_mul, void* y, int32_t yld, int32_t dtype, void* stream);
 /* LayerNorm over the last dim of rows [rows][ld] (first c columns). */
 int rdeic_layernorm(const void* x, int32_t rows, int32_t c, int32_t ld, const float* gamma, const float* beta,
                     float eps, void* y, int32_t yld, int32_t dtype, void* stream);
@@ -93,15 +95,16 @@ int rdeic_layernorm(const void* x, int32_t rows, int32_t c, int32_t ld, const fl
 /* ------------------------------------------------------------- attention
  * softmax(Q K^T * scale) V per (batch, head); Q [b][lq][ldq] with head h at columns
  * h*dh..h*dh+dh-1 (same for K/V/O), i.e. the reference's 'b n (h d)' layout.
- * dh in {16, 32, 64, 128, 256, 512}; any lq, lk >= 1. */
+ * dh in {16, 32, 64}; any lq, lk >= 1. kv_bcast = 1: K/V hold a single batch shared by all
+ * `batch` query batches (the one text context of the cross-attention). */
+int rdeic_attention(const void* q, int32_t ldq, const void* k, int32_t ldk, const void* v, int32_t ldv,
+                    void* o, int32_t ldo, int32_t batch, int32_t heads, int32_t lq, int32_t lk, int32_t dh,
+                    float scale, int32_t kv_bcast, int32_t dtype, void* stream);
 /* materialised-attention helpers (VAE d=512 single-head path): row softmax of s*scale -> p,
  * and batched 2-D transpose. */
 int rdeic_softmax_rows(const float* s, int64_t rows, int32_t cols, float scale, void* p, int32_t dtype, void* stream);
 int rdeic_transpose(const void* in, int32_t rows, int32_t cols, int32_t ldin, void* out, int32_t ldout,
                     int32_t batch, int64_t in_bs, int64_t out_bs, int32_t dtype, void* stream);
-int rdeic_attention(const void* q, int32_t ldq, const void* k, int32_t ldk, const void* v, int32_t ldv,
-                    void* o, int32_t ldo, int32_t batch, int32_t heads, int32_t lq, int32_t lk, int32_t dh,
-                    float scale, int32_t dtype, void* stream);
 
 /* ----------------------------------------------------------- elementwise */
 /* x * gelu(gate) where x = in[:, :c], gate = in[:, c:2c] (GEGLU, attention.py:49-56) */

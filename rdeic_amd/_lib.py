@@ -57,13 +57,14 @@ PROTOTYPES = {
     "rdeic_abi_count": (C.c_int, []),
     "rdeic_conv2d": (C.c_int, [C.POINTER(ConvDesc), _p]),
     "rdeic_groupnorm_ws_floats": (_sz, [_i32, _i32, _i32]),
-    "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p, _i32, _p]),
-    "rdeic_groupnorm_apply": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _p, _i32, _i32, _p]),
+    "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p,
+                                        _i32, _p]),
+    "rdeic_groupnorm_apply": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _f, _p, _i32, _i32, _p]),
     "rdeic_layernorm": (C.c_int, [_p, _i32, _i32, _i32, _p, _p, _f, _p, _i32, _i32, _p]),
     "rdeic_softmax_rows": (C.c_int, [_p, _i64, _i32, _f, _p, _i32, _p]),
     "rdeic_transpose": (C.c_int, [_p, _i32, _i32, _i32, _p, _i32, _i32, _i64, _i64, _i32, _p]),
     "rdeic_attention": (C.c_int, [_p, _i32, _p, _i32, _p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _i32, _f,
-                                  _i32, _p]),
+                                  _i32, _i32, _p]),
     "rdeic_geglu": (C.c_int, [_p, _i32, _i32, _i32, _p, _i32, _i32, _p]),
     "rdeic_nchw_to_nhwc": (C.c_int, [_p, _i32, _i32, _i32, _i32, _f, _f, _p, _i32, _i32, _p]),
     "rdeic_nhwc_to_nchw": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _f, _f, _p, _i32, _p]),

@@ -28,7 +28,7 @@ template <> struct AT<float> { static constexpr int KS = 4; };
 template <typename T, int DH>
 __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ q, int ldq, const T* __restrict__ k, int ldk,
                                                    const T* __restrict__ v, int ldv, T* __restrict__ o, int ldo,
-                                                   int heads, int lq, int lk, float scale_log2) {
+                                                   int heads, int lq, int lk, float scale_log2, int kv_bcast) {
   constexpr int KS = AT<T>::KS;
   constexpr int DP = (DH < KS) ? KS : DH;           // padded head dim for the QK^T contraction
   constexpr int PADE = 16 / sizeof(T);
@@ -50,8 +50,9 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ q, int 
   const int lr = lane & 15, lg = lane >> 4;
 
   const T* qb = q + (long)b * lq * ldq + h * DH;
-  const T* kb = k + (long)b * lk * ldk + h * DH;
-  const T* vb = v + (long)b * lk * ldv + h * DH;
+  const long kvb = kv_bcast ? 0 : b;  // a single K/V batch (shared text context) serves every image
+  const T* kb = k + kvb * lk * ldk + h * DH;
+  const T* vb = v + kvb * lk * ldv + h * DH;
 
   // Q fragments in registers: lane holds Q[q0 + 16*wave + lr][s*KS + (bf16: 8*lg..+8 | f32: lg)]
   const int myq = q0 + wave * 16 + lr;
@@ -228,13 +229,13 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in
 
 template <typename T>
 int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo, int batch,
-                int heads, int lq, int lk, int dh, float scale, hipStream_t s) {
+                int heads, int lq, int lk, int dh, float scale, int kv_bcast, hipStream_t s) {
   dim3 grid((lq + QT - 1) / QT, batch * heads);
   float sl2 = scale * 1.4426950408889634f;
 #define ATTN_CASE(D)                                                                                              \
   case D:                                                                                                         \
     hipLaunchKernelGGL((attn_kernel<T, D>), grid, dim3(256), 0, s, (const T*)q, ldq, (const T*)k, ldk, (const T*)v, \
-                       ldv, (T*)o, ldo, heads, lq, lk, sl2);                                                      \
+                       ldv, (T*)o, ldo, heads, lq, lk, sl2, kv_bcast);                                                      \
     break;
   switch (dh) {
     ATTN_CASE(16)
@@ -250,14 +251,14 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
 
 extern "C" int rdeic_attention(const void* q, int32_t ldq, const void* k, int32_t ldk, const void* v, int32_t ldv,
                                void* o, int32_t ldo, int32_t batch, int32_t heads, int32_t lq, int32_t lk, int32_t dh,
-                               float scale, int32_t dtype, void* stream) {
+                               float scale, int32_t kv_bcast, int32_t dtype, void* stream) {
   if (!q || !k || !v || !o || batch <= 0 || heads <= 0 || lq <= 0 || lk <= 0) return RDEIC_EINVAL;
   const int epc = dtype == 1 ? 8 : 4;
   if (ldq % epc || ldk % epc || ldv % epc || ((uintptr_t)k) % 16 || ((uintptr_t)v) % 16 || ((uintptr_t)q) % 16)
     return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == 1) return launch_attn<bf16>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, s);
-  return launch_attn<float>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, s);
+  if (dtype == 1) return launch_attn<bf16>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
+  return launch_attn<float>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
 }
 
 extern "C" int rdeic_softmax_rows(const float* s, int64_t rows, int32_t cols, float scale, void* p, int32_t dtype,

@@ -5,6 +5,9 @@
 //   pass 1  per (image, pixel-chunk) block: per-channel shifted sums  S1=sum(x-K), S2=sum((x-K)^2)
 //           with K = x[img, pixel 0, ch] (shifted data keeps the fp32 variance well conditioned)
 //   pass 2  per (image, group): combine chunks in a fixed order -> mean, rstd -> per-channel a, b
+// The input may be a two-segment channel concatenation (the UNet decoder's torch.cat of the
+// running activation and the skip), whose groups can straddle the segment boundary: pass 1
+// runs per segment into one per-channel partial buffer, pass 2 is segment-agnostic.
 // Both passes are deterministic (fixed reduction order, no atomics).
 //
 // Replaces GroupNorm32 (ldm/modules/diffusionmodules/util.py:224-226, eps 1e-5, fp32),
@@ -18,19 +21,24 @@ namespace {
 constexpr int GN_CHUNK = 512;  // pixels per pass-1 block
 
 template <typename T>
-__global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x, int hw, int c, int ld, int nchunk,
-                                                         float* __restrict__ part /*[n][nchunk][c][2]*/) {
+__device__ __forceinline__ float load_seg(const T* x0, int c0, int ld0, const T* x1, int ld1, long img_pix, int ch) {
+  return ch < c0 ? to_f32(x0[img_pix * ld0 + ch]) : to_f32(x1[img_pix * ld1 + (ch - c0)]);
+}
+
+// One segment: channels [coff, coff + cs) of the logical c-channel tensor.
+template <typename T>
+__global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x, int hw, int cs, int ld, int coff,
+                                                         int c, int nchunk, float* __restrict__ part) {
   const int img = blockIdx.y, chunk = blockIdx.x;
   const int p0 = chunk * GN_CHUNK;
   const int p1 = min(hw, p0 + GN_CHUNK);
   const T* xi = x + (long)img * hw * ld;
-  // pixel lanes: split the 256 threads into PL pixel lanes when c divides 256
-  int PL = 1;
-  if (c < 256 && 256 % c == 0) PL = 256 / c;
+  int PL = 1;  // pixel lanes when the segment width divides 256
+  if (cs < 256 && 256 % cs == 0) PL = 256 / cs;
   __shared__ float red[2][256];
   const int t = threadIdx.x;
-  const int pl = (PL > 1) ? t / c : 0;
-  for (int ch0 = (PL > 1 ? t % c : t); ch0 < c; ch0 += (PL > 1 ? c : 256)) {
+  if (PL > 1) {
+    const int ch0 = t % cs, pl = t / cs;
     const float K = to_f32(xi[ch0]);
     float s1 = 0.f, s2 = 0.f;
     for (int p = p0 + pl; p < p1; p += PL) {
@@ -38,34 +46,41 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x
       s1 += v;
       s2 += v * v;
     }
-    if (PL > 1) {
-      red[0][t] = s1; red[1][t] = s2;
-      __syncthreads();
-      if (pl == 0) {
-        for (int q = 1; q < PL; ++q) { s1 += red[0][t + q * c]; s2 += red[1][t + q * c]; }
-        float* o = part + (((long)img * nchunk + chunk) * c + ch0) * 2;
-        o[0] = s1; o[1] = s2;
-      }
-      __syncthreads();
-    } else {
-      float* o = part + (((long)img * nchunk + chunk) * c + ch0) * 2;
-      o[0] = s1; o[1] = s2;
+    red[0][t] = s1;
+    red[1][t] = s2;
+    __syncthreads();
+    if (pl == 0) {
+      for (int q = 1; q < PL; ++q) { s1 += red[0][t + q * cs]; s2 += red[1][t + q * cs]; }
+      float* o = part + (((long)img * nchunk + chunk) * c + coff + ch0) * 2;
+      o[0] = s1;
+      o[1] = s2;
     }
-    if (PL > 1) break;
+  } else {
+    for (int ch0 = t; ch0 < cs; ch0 += 256) {
+      const float K = to_f32(xi[ch0]);
+      float s1 = 0.f, s2 = 0.f;
+      for (int p = p0; p < p1; ++p) {
+        float v = to_f32(xi[(long)p * ld + ch0]) - K;
+        s1 += v;
+        s2 += v * v;
+      }
+      float* o = part + (((long)img * nchunk + chunk) * c + coff + ch0) * 2;
+      o[0] = s1;
+      o[1] = s2;
+    }
   }
 }
 
 template <typename T>
-__global__ __launch_bounds__(64) void gn_finalize_kernel(const T* __restrict__ x, int hw, int c, int ld, int groups,
+__global__ __launch_bounds__(64) void gn_finalize_kernel(const T* __restrict__ x0, int c0, int ld0,
+                                                         const T* __restrict__ x1, int ld1, int hw, int c, int groups,
                                                          int nchunk, const float* __restrict__ part, float eps,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float* __restrict__ ab) {
   const int img = blockIdx.y, g = blockIdx.x;
   const int cpg = c / groups;
   const int lane = threadIdx.x;
-  const T* xi = x + (long)img * hw * ld;
-  // pass A: per-channel totals (lane owns channels lane, lane+64, ...) in fixed order
-  double cnt = (double)hw;
+  const float cnt = (float)hw;
   float s1c[8], s2c[8], Kc[8];  // cpg <= 512 -> up to 8 channels per lane
   int nmine = 0;
   for (int j = lane; j < cpg; j += 64, ++nmine) {
@@ -76,22 +91,23 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const T* __restrict__ x
       s1 += pp[0];
       s2 += pp[1];
     }
-    s1c[nmine] = s1; s2c[nmine] = s2; Kc[nmine] = to_f32(xi[ch]);
+    s1c[nmine] = s1;
+    s2c[nmine] = s2;
+    Kc[nmine] = load_seg(x0, c0, ld0, x1, ld1, (long)img * hw, ch);
   }
-  // group mean
   float tot = 0.f;
-  for (int q = 0; q < nmine; ++q) tot += s1c[q] + (float)cnt * Kc[q];
+  for (int q = 0; q < nmine; ++q) tot += s1c[q] + cnt * Kc[q];
   tot = warp_sum(tot);
-  const float n_el = (float)(cnt * cpg);
+  const float n_el = cnt * (float)cpg;
   const float mean = tot / n_el;
   float m2 = 0.f;
   for (int q = 0; q < nmine; ++q) {
     float d = Kc[q] - mean;
-    m2 += s2c[q] + 2.f * d * s1c[q] + (float)cnt * d * d;
+    m2 += s2c[q] + 2.f * d * s1c[q] + cnt * d * d;
   }
   m2 = warp_sum(m2);
-  float var = fmaxf(m2 / n_el, 0.f);
-  float rstd = rsqrtf(var + eps);
+  const float var = fmaxf(m2 / n_el, 0.f);
+  const float rstd = rsqrtf(var + eps);
   for (int j = lane; j < cpg; j += 64) {
     int ch = g * cpg + j;
     float ga = gamma ? gamma[ch] : 1.f, be = beta ? beta[ch] : 0.f;
@@ -101,10 +117,11 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const T* __restrict__ x
   }
 }
 
+// y = silu?(x*a + b) * out_mul, 8-wide when possible
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, int n, int hw, int c, int ld,
-                                                       const float* __restrict__ ab, int silu, T* __restrict__ y,
-                                                       int yld) {
+                                                       const float* __restrict__ ab, int silu, float out_mul,
+                                                       T* __restrict__ y, int yld) {
   long total = (long)n * hw * c;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     long pix = i / c;
@@ -113,7 +130,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
     const float* p = ab + ((long)img * c + ch) * 2;
     float v = to_f32(x[pix * ld + ch]) * p[0] + p[1];
     if (silu) v = silu_f(v);
-    y[pix * yld + ch] = from_f32<T>(v);
+    y[pix * yld + ch] = from_f32<T>(v * out_mul);
   }
 }
 
@@ -143,6 +160,21 @@ __global__ __launch_bounds__(64) void layernorm_kernel(const T* __restrict__ x, 
   }
 }
 
+template <typename T>
+int gn_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1, int32_t ld1, int32_t n, int32_t hw,
+             int32_t groups, float eps, const float* gamma, const float* beta, float* ab, float* ws, hipStream_t s) {
+  const int c = c0 + c1;
+  const int nchunk = (hw + GN_CHUNK - 1) / GN_CHUNK;
+  hipLaunchKernelGGL(gn_partial_kernel<T>, dim3(nchunk, n), dim3(256), 0, s, (const T*)x0, hw, c0, ld0, 0, c, nchunk,
+                     ws);
+  if (c1 > 0)
+    hipLaunchKernelGGL(gn_partial_kernel<T>, dim3(nchunk, n), dim3(256), 0, s, (const T*)x1, hw, c1, ld1, c0, c,
+                       nchunk, ws);
+  hipLaunchKernelGGL(gn_finalize_kernel<T>, dim3(groups, n), dim3(64), 0, s, (const T*)x0, c0, ld0,
+                     (const T*)(x1 ? x1 : x0), c1 > 0 ? ld1 : ld0, hw, c, groups, nchunk, ws, eps, gamma, beta, ab);
+  return launch_status();
+}
+
 }  // namespace
 
 extern "C" size_t rdeic_groupnorm_ws_floats(int32_t n, int32_t hw, int32_t c) {
@@ -150,38 +182,30 @@ extern "C" size_t rdeic_groupnorm_ws_floats(int32_t n, int32_t hw, int32_t c) {
   return (size_t)n * nchunk * c * 2;
 }
 
-extern "C" int rdeic_groupnorm_stats(const void* x, int32_t n, int32_t hw, int32_t c, int32_t ld, int32_t groups,
-                                     float eps, const float* gamma, const float* beta, float* ab, float* ws,
-                                     int32_t dtype, void* stream) {
-  if (!x || !ab || !ws || n <= 0 || hw <= 0 || c <= 0 || groups <= 0 || c % groups != 0 || c / groups > 512)
+extern "C" int rdeic_groupnorm_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1, int32_t ld1,
+                                     int32_t n, int32_t hw, int32_t groups, float eps, const float* gamma,
+                                     const float* beta, float* ab, float* ws, int32_t dtype, void* stream) {
+  const int c = c0 + c1;
+  if (!x0 || !ab || !ws || n <= 0 || hw <= 0 || c0 <= 0 || c1 < 0 || (c1 > 0 && !x1) || groups <= 0 ||
+      c % groups != 0 || c / groups > 512)
     return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  int nchunk = (hw + GN_CHUNK - 1) / GN_CHUNK;
-  dim3 g1(nchunk, n), g2(groups, n);
-  if (dtype == 1) {
-    hipLaunchKernelGGL(gn_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)x, hw, c, ld, nchunk, ws);
-    hipLaunchKernelGGL(gn_finalize_kernel<bf16>, g2, dim3(64), 0, s, (const bf16*)x, hw, c, ld, groups, nchunk, ws,
-                       eps, gamma, beta, ab);
-  } else {
-    hipLaunchKernelGGL(gn_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)x, hw, c, ld, nchunk, ws);
-    hipLaunchKernelGGL(gn_finalize_kernel<float>, g2, dim3(64), 0, s, (const float*)x, hw, c, ld, groups, nchunk,
-                       ws, eps, gamma, beta, ab);
-  }
-  return launch_status();
+  if (dtype == 1) return gn_stats<bf16>(x0, c0, ld0, x1, c1, ld1, n, hw, groups, eps, gamma, beta, ab, ws, s);
+  return gn_stats<float>(x0, c0, ld0, x1, c1, ld1, n, hw, groups, eps, gamma, beta, ab, ws, s);
 }
 
 extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32_t c, int32_t ld, const float* ab,
-                                     int32_t silu, void* y, int32_t yld, int32_t dtype, void* stream) {
+                                     int32_t silu, float out_mul, void* y, int32_t yld, int32_t dtype, void* stream) {
   if (!x || !ab || !y || n <= 0 || hw <= 0 || c <= 0) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   long total = (long)n * hw * c;
-  int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   if (dtype == 1)
     hipLaunchKernelGGL(gn_apply_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld, ab, silu,
-                       (bf16*)y, yld);
+                       out_mul, (bf16*)y, yld);
   else
     hipLaunchKernelGGL(gn_apply_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, n, hw, c, ld, ab, silu,
-                       (float*)y, yld);
+                       out_mul, (float*)y, yld);
   return launch_status();
 }
 

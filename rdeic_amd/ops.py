@@ -188,23 +188,27 @@ def gemm_batched(a: torch.Tensor, b_nk: torch.Tensor, out: torch.Tensor, *, batc
     return out
 
 
-def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float) -> torch.Tensor:
-    """Per-(image, channel) affine [n, c, 2] such that GroupNorm(x) = x*a + b."""
-    n, h, w, c = x.shape
-    ld = pix_ld(x)
+def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float,
+                  x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-(image, channel) affine [n, c, 2] such that GroupNorm(cat(x, x2)) = x*a + b."""
+    n, h, w, c0 = x.shape
+    ld0 = pix_ld(x)
+    c1, ld1 = (x2.shape[3], pix_ld(x2)) if x2 is not None else (0, 0)
+    c = c0 + c1
     ws = torch.empty(int(_lib.load().rdeic_groupnorm_ws_floats(n, h * w, c)), dtype=torch.float32, device=x.device)
     ab = torch.empty((n, c, 2), dtype=torch.float32, device=x.device)
-    call("rdeic_groupnorm_stats", x.data_ptr(), n, h * w, c, ld, groups, float(eps), gamma.data_ptr(),
-         beta.data_ptr(), ab.data_ptr(), ws.data_ptr(), dt_code(x), stream_ptr())
+    call("rdeic_groupnorm_stats", x.data_ptr(), c0, ld0, _ptr(x2), c1, ld1, n, h * w, groups, float(eps),
+         gamma.data_ptr(), beta.data_ptr(), ab.data_ptr(), ws.data_ptr(), dt_code(x), stream_ptr())
     return ab
 
 
-def group_norm_apply(x: torch.Tensor, ab: torch.Tensor, silu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def group_norm_apply(x: torch.Tensor, ab: torch.Tensor, silu: bool, out: Optional[torch.Tensor] = None,
+                     out_mul: float = 1.0) -> torch.Tensor:
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)
-    call("rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(), int(silu), out.data_ptr(),
-         pix_ld(out), dt_code(x), stream_ptr())
+    call("rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(), int(silu), float(out_mul),
+         out.data_ptr(), pix_ld(out), dt_code(x), stream_ptr())
     return out
 
 
@@ -219,10 +223,12 @@ def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: fl
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, *, batch: int, heads: int,
-              lq: int, lk: int, dh: int, scale: float) -> torch.Tensor:
-    """Flash attention over [batch*lq, heads*dh]-layout projections (row strides from the tensors)."""
+              lq: int, lk: int, dh: int, scale: float, kv_bcast: bool = False) -> torch.Tensor:
+    """Flash attention over [batch*lq, heads*dh]-layout projections (row strides from the tensors).
+    kv_bcast: K/V hold one batch shared by every query batch."""
     call("rdeic_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
-         out.data_ptr(), out.stride(0), batch, heads, lq, lk, dh, float(scale), dt_code(q), stream_ptr())
+         out.data_ptr(), out.stride(0), batch, heads, lq, lk, dh, float(scale), int(kv_bcast), dt_code(q),
+         stream_ptr())
     return out
 
 

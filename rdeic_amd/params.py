@@ -1,0 +1,112 @@
+"""Parameter store: reference-named fp32 master tensors on the device + packed MFMA weights.
+
+Names are the reference RDEIC state_dict keys (model.diffusion_model.*, control_model.*,
+first_stage_model.*, preprocess_model.*), so a reference checkpoint loads unchanged
+(load_state_dict) and the synthetic generator (rdeic_amd/weights.py) is keyed identically.
+Packing (rdeic_pack_conv_weight) runs on device once per layer and is cached.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, Optional, Sequence, Tuple
+
+import torch
+
+from . import ops
+from . import weights as W
+
+
+class ParamStore:
+    def __init__(self, compute_dtype=torch.bfloat16, device="cuda"):
+        self.compute_dtype = compute_dtype
+        self.device = torch.device(device)
+        self.shapes: Dict[str, Tuple[int, ...]] = {}
+        self.t: Dict[str, torch.Tensor] = {}
+        self._packed: Dict[tuple, ops.ConvParams] = {}
+
+    # ------------------------------------------------------------ declaration
+    def declare(self, name: str, shape: Sequence[int]):
+        shape = tuple(int(s) for s in shape)
+        if name in self.shapes and self.shapes[name] != shape:
+            raise ValueError(f"{name} declared twice with different shapes")
+        self.shapes[name] = shape
+
+    def declare_conv(self, prefix: str, cout: int, cin: int, k: int, bias: bool = True):
+        self.declare(prefix + ".weight", (cout, cin, k, k))
+        if bias:
+            self.declare(prefix + ".bias", (cout,))
+
+    def declare_linear(self, prefix: str, cout: int, cin: int, bias: bool = True):
+        self.declare(prefix + ".weight", (cout, cin))
+        if bias:
+            self.declare(prefix + ".bias", (cout,))
+
+    def declare_norm(self, prefix: str, c: int):
+        self.declare(prefix + ".weight", (c,))
+        self.declare(prefix + ".bias", (c,))
+
+    # ------------------------------------------------------------ materialisation
+    def init_synthetic(self, global_seed: int = W.GLOBAL_SEED):
+        """Counter-based synthetic weights generated on device (bit-identical to the oracle's)."""
+        for name, shape in self.shapes.items():
+            scale, offset = W.init_spec(name, shape)
+            t = torch.empty(shape, dtype=torch.float32, device=self.device)
+            ops.fill_uniform(t, W.param_seed(name, global_seed), scale, offset)
+            self.t[name] = t
+        self._packed.clear()
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        missing = [n for n in self.shapes if n not in sd]
+        if strict and missing:
+            raise KeyError(f"missing parameters: {missing[:8]}{' ...' if len(missing) > 8 else ''}")
+        for name, shape in self.shapes.items():
+            if name not in sd:
+                continue
+            v = sd[name]
+            if tuple(v.shape) != shape:
+                raise ValueError(f"{name}: checkpoint shape {tuple(v.shape)} != {shape}")
+            self.t[name] = v.detach().to(device=self.device, dtype=torch.float32).contiguous()
+        self._packed.clear()
+
+    def names(self) -> Iterable[str]:
+        return self.shapes.keys()
+
+    def get(self, name: str) -> torch.Tensor:
+        return self.t[name]
+
+    def has(self, name: str) -> bool:
+        return name in self.shapes
+
+    # ------------------------------------------------------------ packed weights
+    def conv(self, prefix: str, stride: int = 1, pad: Optional[int] = None, dtype=None,
+             scale: float = 1.0) -> ops.ConvParams:
+        dtype = dtype or self.compute_dtype
+        key = (prefix, stride, pad, dtype, scale)
+        p = self._packed.get(key)
+        if p is None:
+            w = self.t[prefix + ".weight"]
+            b = self.t.get(prefix + ".bias")
+            if scale != 1.0:
+                w, b = w * scale, (None if b is None else b * scale)
+            k = w.shape[-1] if w.dim() == 4 else 1
+            p = ops.ConvParams.pack(w, b, stride=stride, pad=(k // 2 if pad is None else pad), dtype=dtype)
+            self._packed[key] = p
+        return p
+
+    def conv_cat(self, prefixes: Sequence[str], dtype=None) -> ops.ConvParams:
+        """Several layers with the same input stacked along cout (one GEMM: q|k|v, k|v, emb_layers)."""
+        dtype = dtype or self.compute_dtype
+        key = (tuple(prefixes), "cat", dtype)
+        p = self._packed.get(key)
+        if p is None:
+            ws, bs = [], []
+            for pre in prefixes:
+                w = self.t[pre + ".weight"]
+                ws.append(w if w.dim() == 4 else w[:, :, None, None])
+                b = self.t.get(pre + ".bias")
+                bs.append(b if b is not None else torch.zeros(w.shape[0], device=self.device))
+            any_bias = any(self.t.get(pre + ".bias") is not None for pre in prefixes)
+            w = torch.cat(ws, 0)
+            p = ops.ConvParams.pack(w, torch.cat(bs, 0) if any_bias else None, stride=1, pad=w.shape[-1] // 2,
+                                    dtype=dtype)
+            self._packed[key] = p
+        return p

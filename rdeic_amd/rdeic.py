@@ -1,0 +1,210 @@
+"""RDEIC codec model — the reference's model/rdeic.py API surface on the MI355X path.
+
+API parity (model/rdeic.py, ldm/models/diffusion/ddpm.py):
+  apply_condition_compress(x, stream_path, H, W) -> bpp          rdeic.py:659-669
+  apply_condition_decompress(stream_path) -> (c_latent, guide_hint) rdeic.py:671-676
+  q_sample(x_start, t, noise)                                      ddpm.py:357-360
+  apply_model(x_noisy, t, cond) -> eps                             rdeic.py:688-698
+  decode_first_stage(z)                                            ddpm.py:835-844
+  alphas_cumprod & co. (register_schedule, ddpm.py:139-193), used_timesteps, parameterization,
+  scale_factor, device, preprocess_model.update(force=True), load_state_dict(state_dict).
+Tensors crossing this API are the reference's NCHW fp32; internally everything is NHWC and the
+batched fast path (`codec_images`) never converts layouts between stages.
+Text conditioning (OpenCLIP, out of scope) is supplied as a context tensor [1 or B, 77, 1024].
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import bitstream, ops
+from .compression import Compression
+from .config import default_config
+from .params import ParamStore
+from .unet import NoiseEstimator
+from .vae import AutoencoderKL
+
+
+def make_schedule(timesteps: int, linear_start: float, linear_end: float) -> Dict[str, torch.Tensor]:
+    """register_schedule('linear') buffers: fp64 numpy math, stored fp32 (ddpm.py:139-193, util.py:21-50)."""
+    betas = (torch.linspace(linear_start ** 0.5, linear_end ** 0.5, timesteps, dtype=torch.float64) ** 2).numpy()
+    alphas = 1.0 - betas
+    ac = np.cumprod(alphas, axis=0)
+    ac_prev = np.append(1.0, ac[:-1])
+    f = lambda a: torch.tensor(a, dtype=torch.float32)  # noqa: E731
+    return dict(betas=f(betas), alphas_cumprod=f(ac), alphas_cumprod_prev=f(ac_prev),
+                sqrt_alphas_cumprod=f(np.sqrt(ac)), sqrt_one_minus_alphas_cumprod=f(np.sqrt(1.0 - ac)),
+                log_one_minus_alphas_cumprod=f(np.log(1.0 - ac)), sqrt_recip_alphas_cumprod=f(np.sqrt(1.0 / ac)),
+                sqrt_recipm1_alphas_cumprod=f(np.sqrt(1.0 / ac - 1)),
+                posterior_variance=f(betas * (1.0 - ac_prev) / (1.0 - ac)),
+                posterior_log_variance_clipped=f(np.log(np.maximum(betas * (1.0 - ac_prev) / (1.0 - ac), 1e-20))),
+                posterior_mean_coef1=f(betas * np.sqrt(ac_prev) / (1.0 - ac)),
+                posterior_mean_coef2=f((1.0 - ac_prev) * np.sqrt(alphas) / (1.0 - ac)))
+
+
+class RDEIC:
+    parameterization = "eps"
+
+    def __init__(self, config: Optional[dict] = None, compute_dtype=torch.bfloat16, device="cuda"):
+        cfg = config or default_config()
+        self.cfg = cfg
+        self.store = ParamStore(compute_dtype, device)
+        self.control_model = NoiseEstimator(self.store, cfg["unet"], cfg["control"])
+        self.first_stage_model = AutoencoderKL(self.store, cfg["ddconfig"], cfg["embed_dim"])
+        self.preprocess_model = Compression(self.store, **cfg["compression"])
+        self.scale_factor = float(cfg["scale_factor"])
+        self.num_timesteps = int(cfg["timesteps"])
+        self.used_timesteps = int(cfg["used_timesteps"])
+        self.channels = 4
+        sched = make_schedule(self.num_timesteps, cfg["linear_start"], cfg["linear_end"])
+        self._sched_cpu = sched
+        self.device = torch.device(device)
+        for k, v in sched.items():
+            setattr(self, k, v.to(self.device))
+
+    # ------------------------------------------------------------------ weights
+    @property
+    def compute_dtype(self):
+        return self.store.compute_dtype
+
+    def init_synthetic(self, seed: Optional[int] = None):
+        from . import weights as W
+        self.store.init_synthetic(W.GLOBAL_SEED if seed is None else seed)
+        self.preprocess_model._en = None
+        return self
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        """Load reference-named weights (e.g. a RDEIC checkpoint's state_dict). Non-parameter buffers of the
+        reference (schedules, entropy tables, scale_list, cond_stage_model) are ignored."""
+        self.store.load_state_dict({k: v for k, v in sd.items() if k in self.store.shapes}, strict=strict)
+        self.preprocess_model._en = None
+        return self
+
+    def param_shapes(self):
+        return dict(self.store.shapes)
+
+    # ------------------------------------------------------------------ internal NHWC stages
+    def encode_images_nhwc(self, img_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 [B,H,W,3] (device) -> h = 0.18215 * Encoder.forward_hc(x*2-1), NHWC compute dtype."""
+        B, H, W_, _ = img_u8.shape
+        x = torch.empty((B, H, W_, 3), dtype=self.compute_dtype, device=img_u8.device)
+        ops.call("rdeic_image_u8_to_nhwc", img_u8.contiguous().data_ptr(), B, H, W_, x.data_ptr(), 3, ops.dt_code(x),
+                 ops.stream_ptr())
+        return self.first_stage_model.encode_hc(x, out_mul=self.scale_factor)
+
+    def encode_nchw_nhwc(self, x: torch.Tensor) -> torch.Tensor:
+        """x in [0,1] NCHW fp32 -> h (apply_condition_compress's x*2-1 fused into the layout conversion)."""
+        xh = ops.nchw_to_nhwc(x.to(self.device), self.compute_dtype, mul=2.0, add=-1.0)
+        return self.first_stage_model.encode_hc(xh, out_mul=self.scale_factor)
+
+    def q_sample_nhwc(self, x0: torch.Tensor, t: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
+        B = x0.shape[0]
+        t = t.to(self.device).long()
+        a = self.sqrt_alphas_cumprod[t].contiguous()
+        b = self.sqrt_one_minus_alphas_cumprod[t].contiguous()
+        out = torch.empty_like(x0)
+        ops.call("rdeic_axpby", x0.contiguous().data_ptr(), noise.contiguous().data_ptr(), B, x0[0].numel(),
+                 a.data_ptr(), b.data_ptr(), out.data_ptr(), ops.stream_ptr())
+        return out
+
+    def eps_nhwc(self, x: torch.Tensor, t: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor):
+        return self.control_model.forward(x, guide_hint, t, context.to(self.device))
+
+    def decode_nhwc(self, z: torch.Tensor, out_f32: bool = True) -> torch.Tensor:
+        """z: fp32 NHWC latent sample -> decoder output NHWC [B,8h,8w,3] (1/scale_factor fused)."""
+        B = z.shape[0]
+        zs = torch.empty_like(z)
+        inv = torch.full((B,), 1.0 / self.scale_factor, dtype=torch.float32, device=z.device)
+        zero = torch.zeros((B,), dtype=torch.float32, device=z.device)
+        ops.call("rdeic_axpby", z.contiguous().data_ptr(), z.contiguous().data_ptr(), B, z[0].numel(), inv.data_ptr(),
+                 zero.data_ptr(), zs.data_ptr(), ops.stream_ptr())
+        zc = ops.cast(zs, self.compute_dtype)
+        return self.first_stage_model.decode(zc, out_f32=out_f32)
+
+    def to_image_u8(self, x: torch.Tensor) -> torch.Tensor:
+        B, H, W_, C = x.shape
+        img = torch.empty((B, H, W_, 3), dtype=torch.uint8, device=x.device)
+        ops.call("rdeic_nhwc_to_image_u8", x.data_ptr(), B, H, W_, ops.pix_ld(x), img.data_ptr(), ops.dt_code(x),
+                 ops.stream_ptr())
+        return img
+
+    # ------------------------------------------------------------------ reference API
+    @torch.no_grad()
+    def apply_condition_compress(self, x: torch.Tensor, stream_path: str, H: int, W: int) -> float:
+        """x: [1,3,H,W] in [0,1]. Writes the bitstream file, returns bpp = 8*filesize/(H*W)."""
+        if x.shape[0] != 1:
+            raise ValueError("apply_condition_compress codes one image per file (the reference's decompress "
+                             "supports batch 1 only); use compress_images for batches")
+        h = self.encode_nchw_nhwc(x)
+        out = self.preprocess_model.compress(h)[0]
+        with Path(stream_path).open("wb") as f:
+            bitstream.write_body(f, out["shape"], out["strings"])
+        size = bitstream.filesize(stream_path)
+        return float(size) * 8 / (H * W)
+
+    @torch.no_grad()
+    def apply_condition_decompress(self, stream_path: str):
+        with Path(stream_path).open("rb") as f:
+            strings, shape = bitstream.read_body(f)
+        c_lat, hint = self.preprocess_model.decompress([strings], shape, device=self.device)
+        return ops.nhwc_to_nchw(c_lat), ops.nhwc_to_nchw(hint)
+
+    def q_sample(self, x_start: torch.Tensor, t: torch.Tensor, noise: Optional[torch.Tensor] = None):
+        if noise is None:
+            noise = torch.randn_like(x_start)
+        B, C, H, W_ = x_start.shape
+        out = self.q_sample_nhwc(x_start.float().contiguous(), t, noise.float().contiguous().to(x_start.device))
+        return out  # elementwise: layout-agnostic, returned in the caller's (NCHW) layout
+
+    @torch.no_grad()
+    def apply_model(self, x_noisy: torch.Tensor, t: torch.Tensor, cond: dict) -> torch.Tensor:
+        ctx = torch.cat(cond["c_crossattn"], 1)
+        x = ops.nchw_to_nhwc(x_noisy.float().to(self.device), torch.float32)
+        hint = cond["guide_hint"]
+        hint_nhwc = ops.nchw_to_nhwc(hint.float().to(self.device), self.compute_dtype)
+        eps = self.eps_nhwc(x, t.to(self.device), hint_nhwc, ctx)
+        return ops.nhwc_to_nchw(eps)
+
+    @torch.no_grad()
+    def decode_first_stage(self, z: torch.Tensor) -> torch.Tensor:
+        zn = ops.nchw_to_nhwc(z.float().to(self.device), torch.float32)
+        return ops.nhwc_to_nchw(self.decode_nhwc(zn, out_f32=True))
+
+    # ------------------------------------------------------------------ batched codec fast path
+    @torch.no_grad()
+    def compress_images(self, img_u8: torch.Tensor) -> List[bytes]:
+        """uint8 [B,H,W,3] (H, W multiples of 64) -> B bitstream bodies (reference file format)."""
+        h = self.encode_images_nhwc(img_u8.to(self.device))
+        return [bitstream.pack_body(o["shape"], o["strings"]) for o in self.preprocess_model.compress(h)]
+
+    @torch.no_grad()
+    def decompress_bodies(self, bodies: Sequence[bytes]):
+        parsed = [bitstream.unpack_body(b) for b in bodies]
+        shape = parsed[0][1]
+        if any(p[1] != shape for p in parsed):
+            raise ValueError("batched decompress needs one latent shape per batch")
+        return self.preprocess_model.decompress([p[0] for p in parsed], shape, device=self.device)
+
+    @torch.no_grad()
+    def relay_sample_nhwc(self, c_latent: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor,
+                          noise: torch.Tensor, steps: int) -> torch.Tensor:
+        """x_T = q_sample(c_latent, used_timesteps-1, noise); relay DDIM (eta=0) for `steps` steps."""
+        from .ddim_sampler_relay import DDIMSampler
+        B = c_latent.shape[0]
+        t = torch.full((B,), self.used_timesteps - 1, dtype=torch.long, device=self.device)
+        x = self.q_sample_nhwc(c_latent, t, noise)
+        return DDIMSampler(self).sample_nhwc(steps, x, guide_hint, context)
+
+    @torch.no_grad()
+    def codec_images(self, img_u8: torch.Tensor, context: torch.Tensor, noise_nchw: torch.Tensor, steps: int = 2):
+        """The full hot path on a batch: compress -> bytes -> decompress -> relay denoise -> VAE decode -> u8.
+        Returns (uint8 [B,H,W,3] on device, list of bitstream bodies)."""
+        bodies = self.compress_images(img_u8)
+        c_lat, hint = self.decompress_bodies(bodies)
+        noise = ops.nchw_to_nhwc(noise_nchw.float().to(self.device), torch.float32)
+        z = self.relay_sample_nhwc(c_lat, hint, context, noise, steps)
+        return self.to_image_u8(self.decode_nhwc(z, out_f32=True)), bodies
