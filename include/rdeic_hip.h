@@ -72,6 +72,9 @@ typedef struct rdeic_conv_desc {
 } rdeic_conv_desc;
 
 int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
+/* 1 (default): bf16 convs without a GN prologue use the LDS-DMA pipelined kernel; 0: the
+ * register-staged kernel everywhere (A/B timing, debugging). Returns the previous value. */
+int rdeic_set_conv_path(int32_t path);
 
 /* --------------------------------------------------------- normalisation
  * GroupNorm statistics over NHWC x[n][hw][ld] (first c channels), groups of c/g
@@ -87,7 +90,8 @@ int rdeic_groupnorm_stats(const void* x0, int32_t c0, int32_t ld0, const void* x
 /* y = silu?(x*a + b) * out_mul materialised (NHWC), where the consumer is not a conv
  * (e.g. the VAE encoder's c = swish(norm_out(h)), followed by the 0.18215 latent scale). */
 int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32_t c, int32_t ld, const float* ab,
-                          int32_t silu, float out_mul, void* y, int32_t yld, int32_t dtype, void* stream);
+                          int32_t ab_c, int32_t silu, float out_mul, void* y, int32_t yld, int32_t dtype,
+                          void* stream);
 /* LayerNorm over the last dim of rows [rows][ld] (first c columns). */
 int rdeic_layernorm(const void* x, int32_t rows, int32_t c, int32_t ld, const float* gamma, const float* beta,
                     float eps, void* y, int32_t yld, int32_t dtype, void* stream);
@@ -131,6 +135,8 @@ int rdeic_image_u8_to_nhwc(const uint8_t* img, int32_t n, int32_t h, int32_t w, 
                            int32_t dtype, void* stream);
 int rdeic_nhwc_to_image_u8(const void* x, int32_t n, int32_t h, int32_t w, int32_t ld, uint8_t* img,
                            int32_t dtype, void* stream);
+/* per-image MSE of two uint8 image batches (n images of per_img bytes) -> out[n] (PSNR metric) */
+int rdeic_image_mse(const uint8_t* a, const uint8_t* b, int32_t n, int64_t per_img, float* out, void* stream);
 /* counter-based synthetic weights: out[i] = ((splitmix64(seed + i) >> 40) - 2^23) * scale + offset */
 int rdeic_fill_uniform(float* out, int64_t count, uint64_t seed, float scale, float offset, void* stream);
 /* fp32 -> packed conv weight [cout][wld] (zero tail), from torch layout [cout][cin][kh][kw] */

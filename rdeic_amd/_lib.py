@@ -59,7 +59,8 @@ PROTOTYPES = {
     "rdeic_groupnorm_ws_floats": (_sz, [_i32, _i32, _i32]),
     "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p,
                                         _i32, _p]),
-    "rdeic_groupnorm_apply": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _f, _p, _i32, _i32, _p]),
+    "rdeic_groupnorm_apply": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _i32, _f, _p, _i32, _i32, _p]),
+    "rdeic_set_conv_path": (C.c_int, [_i32]),
     "rdeic_layernorm": (C.c_int, [_p, _i32, _i32, _i32, _p, _p, _f, _p, _i32, _i32, _p]),
     "rdeic_softmax_rows": (C.c_int, [_p, _i64, _i32, _f, _p, _i32, _p]),
     "rdeic_transpose": (C.c_int, [_p, _i32, _i32, _i32, _p, _i32, _i32, _i64, _i64, _i32, _p]),
@@ -74,6 +75,7 @@ PROTOTYPES = {
     "rdeic_silu_f32": (C.c_int, [_p, _p, _i64, _p]),
     "rdeic_image_u8_to_nhwc": (C.c_int, [_p, _i32, _i32, _i32, _p, _i32, _i32, _p]),
     "rdeic_nhwc_to_image_u8": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _p]),
+    "rdeic_image_mse": (C.c_int, [_p, _p, _i32, _i64, _p, _p]),
     "rdeic_fill_uniform": (C.c_int, [_p, _i64, _u64, _f, _f, _p]),
     "rdeic_pack_conv_weight": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
     "rdeic_cast": (C.c_int, [_p, _i32, _p, _i32, _i64, _p]),

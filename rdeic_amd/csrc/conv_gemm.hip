@@ -325,6 +325,197 @@ int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
   return launch_status();
 }
 
+// ============================================================================================
+// bf16 main path: LDS-DMA (global_load_lds_dwordx4) staged implicit GEMM with a STAGES-deep
+// ring. Each lane's 16-byte source address is computed per k-tile (the implicit-im2col gather,
+// zero page for padding / tails), so the A operand never passes through VGPRs; the LDS image is
+// lane-linear per wave instruction ([row][8 x 16-byte slots], 128-byte rows) and XOR-swizzled
+// through the SOURCE address (slot s of row r holds k-chunk s ^ (r & 7)), read back with the same
+// XOR so the MFMA fragment reads (ds_read_b128) spread over the banks. Waits are counted
+// (s_waitcnt vmcnt(N) + raw s_barrier), so STAGES-2 tiles stay in flight across each barrier.
+// No GroupNorm prologue here: GN+SiLU inputs are materialised by rdeic_groupnorm_apply first.
+// ============================================================================================
+__device__ uint4 g_zero_page[64];  // 1 KiB of zeros: source of every padded / out-of-range chunk
+int g_conv_path = 1;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WGM, int WGN, int STAGES>
+__global__ __launch_bounds__(WGM * WGN * 64) void conv_glds_kernel(ConvArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int NT = NW * 64;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int AI = BM / NW / 8;  // glds instructions per lane per stage (A)
+  constexpr int BI = BN / NW / 8;  // (B)
+  constexpr int PER = AI + BI;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave split");
+  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
+
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  if (gridDim.z > 1) {
+    const long z = blockIdx.z;
+    a.in0 += z * a.in_bs * 2; a.in1 += z * a.in_bs * 2;
+    a.weight += z * a.w_bs * 2;
+    a.out += z * a.out_bs * (a.out_f32 ? 4 : 2);
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int hw_o = a.ho * a.wo;
+  const int hin = a.up2 ? 2 * a.h : a.h, win = a.up2 ? 2 * a.w : a.w;
+  const int lrow8 = lane >> 3;
+  const int g = (lane & 7) ^ lrow8;  // this lane's k-chunk (fixed for all k-tiles and rows)
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
+
+  int r_img[AI], r_iy[AI], r_ix[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int m = m0 + wave * (BM / NW) + j * 8 + lrow8;
+    if (m < a.M) {
+      int img = m / hw_o, rem = m - img * hw_o;
+      int oy = rem / a.wo, ox = rem - oy * a.wo;
+      r_img[j] = img;
+      r_iy[j] = oy * a.stride - a.pad_t;
+      r_ix[j] = ox * a.stride - a.pad_l;
+    } else {
+      r_img[j] = -1; r_iy[j] = 0; r_ix[j] = 0;
+    }
+  }
+  const char* b_row[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int nn = n0 + wave * (BN / NW) + j * 8 + lrow8;
+    b_row[j] = nn < a.cout ? a.weight + ((long)nn * a.wld + g * 8) * 2 : nullptr;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    char* sb = lds + buf * STAGE;
+    const int k0 = kt * 64 + g * 8;
+    const bool kval = k0 < a.ktot;
+    int tap = kval ? k0 / a.cin : 0;
+    int c = k0 - tap * a.cin;
+    int ky = tap / a.kw, kx = tap - ky * a.kw;
+    const char* base; int ld, cs;
+    if (c < a.c0) { base = a.in0; ld = a.ld0; cs = c; } else { base = a.in1; ld = a.ld1; cs = c - a.c0; }
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      int iy = r_iy[j] + ky, ix = r_ix[j] + kx;
+      const bool ok = kval && r_img[j] >= 0 && iy >= 0 && iy < hin && ix >= 0 && ix < win;
+      if (a.up2) { iy >>= 1; ix >>= 1; }
+      const char* src = ok ? base + ((((long)r_img[j] * a.h + iy) * a.w + ix) * ld + cs) * 2 : zp;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(sb + (wave * (BM / NW) + j * 8) * 128),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const char* src = b_row[j] ? b_row[j] + (long)kt * 128 : zp;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src, (__attribute__((address_space(3))) void*)(sb + A_BYTES + (wave * (BN / NW) + j * 8) * 128),
+          16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lq = lane >> 4;
+  const int nk = a.nk;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int after = min(STAGES - 2, nk - 1 - kt);  // stages issued after tile kt
+    if constexpr (STAGES >= 4) {
+      if (after >= 2) wait_vmcnt<2 * PER>();
+      else if (after == 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+    } else if constexpr (STAGES == 3) {
+      if (after >= 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* Ab = lds + (kt % STAGES) * STAGE + (wm * WTM + lr) * 128;
+    const char* Bb = lds + (kt % STAGES) * STAGE + A_BYTES + (wn * WTN + lr) * 128;
+    const int sw = lr & 7;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int slot = ((s * 4 + lq) ^ sw) * 16;
+      bf16x8 af[TM], bfv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * 128 + slot);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * 128 + slot);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // ---------------- epilogue (same semantics as conv_kernel)
+  const bool of32 = a.out_f32;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
+      if (m >= a.M) continue;
+      const int img = m / hw_o;
+      int oy = 0, ox = 0;
+      if (a.out_mode == 1) { int rem = m - img * hw_o; oy = rem / a.wo; ox = rem - oy * a.wo; }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nn = n0 + wn * WTN + j * 16 + lr;
+        if (nn >= a.cout) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v += a.bias[nn];
+        if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
+        v = apply_act(v, a.act, a.act_param);
+        long oidx, ridx;
+        if (a.out_mode == 1) {
+          int c = nn >> 2, dy = (nn >> 1) & 1, dx = nn & 1;
+          long p = ((long)img * (2 * a.ho) + (2 * oy + dy)) * (2 * a.wo) + (2 * ox + dx);
+          oidx = p * a.out_ld + c;
+          ridx = p * a.res_ld + c;
+        } else {
+          oidx = (long)m * a.out_ld + nn;
+          ridx = (long)m * a.res_ld + nn;
+        }
+        if (a.res) v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const bf16*>(a.res)[ridx]);
+        if (of32) reinterpret_cast<float*>(a.out)[oidx] = v;
+        else reinterpret_cast<bf16*>(a.out)[oidx] = from_f32<bf16>(v);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int STAGES>
+int launch_glds(const ConvArgs& a, hipStream_t s) {
+  dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
+  size_t lds = (size_t)STAGES * (BM + BN) * 128;
+  hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WGM, WGN, STAGES>), grid, dim3(WGM * WGN * 64), lds, s, a);
+  return launch_status();
+}
+
 }  // namespace
 
 extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
@@ -362,6 +553,12 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
   if (d->c1) vec = vec && (d->c1 % epc == 0) && (d->ld1 % epc == 0) && (((uintptr_t)d->in1) % 16 == 0);
   if (((uintptr_t)d->weight) % 16 != 0) return RDEIC_EINVAL;
 
+  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path != 0) {
+    // LDS-DMA pipelined path (wld % 64 == 0 and 16-byte aligned rows are guaranteed above)
+    if (d->cout % 128 != 0 && d->cout % 64 == 0) return launch_glds<128, 64, 2, 2, 3>(a, s);
+    if (a.M <= 8192) return launch_glds<64, 128, 2, 2, 3>(a, s);
+    return launch_glds<128, 128, 2, 2, 3>(a, s);
+  }
   if (d->dtype == 1) {
     if (d->cout <= 16) return launch_cfg<bf16, 128, 16, 4, 1>(a, vec, s);
     if (d->cout <= 32) return launch_cfg<bf16, 128, 32, 4, 1>(a, vec, s);
@@ -372,4 +569,10 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
     if (d->cout <= 16) return launch_cfg<float, 64, 16, 4, 1>(a, vec, s);
     return launch_cfg<float, 64, 64, 2, 2>(a, vec, s);
   }
+}
+
+extern "C" int rdeic_set_conv_path(int32_t path) {
+  int prev = g_conv_path;
+  g_conv_path = path;
+  return prev;
 }

@@ -292,3 +292,31 @@ extern "C" int rdeic_cast(const void* in, int32_t in_dtype, void* out, int32_t o
     hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(g), dim3(256), 0, s, (const bf16*)in, (bf16*)out, (long)count);
   return launch_status();
 }
+
+namespace {
+// per-image mean squared error between two uint8 images (PSNR metric row of the bench / CLI)
+__global__ __launch_bounds__(256) void image_mse_kernel(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                                        long per_img, float* __restrict__ out) {
+  const long base = (long)blockIdx.x * per_img;
+  double s = 0.0;
+  for (long i = threadIdx.x; i < per_img; i += 256) {
+    double d = (double)a[base + i] - (double)b[base + i];
+    s += d * d;
+  }
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = (float)(red[0] / (double)per_img);
+}
+}  // namespace
+
+extern "C" int rdeic_image_mse(const uint8_t* a, const uint8_t* b, int32_t n, int64_t per_img, float* out,
+                               void* stream) {
+  if (!a || !b || !out || n <= 0 || per_img <= 0) return RDEIC_EINVAL;
+  hipLaunchKernelGGL(image_mse_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, a, b, (long)per_img, out);
+  return launch_status();
+}

@@ -71,6 +71,52 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x
   }
 }
 
+// 16-byte vectorised pass 1 for bf16 (segment width a multiple of 8, at most 2048 channels):
+// thread = one 8-channel chunk of pixels pl, pl+PL, ...; pixel lanes reduced in a fixed order.
+__global__ __launch_bounds__(256) void gn_partial_vec_kernel(const bf16* __restrict__ x, int hw, int cs, int ld,
+                                                             int coff, int c, int nchunk, float* __restrict__ part) {
+  const int img = blockIdx.y, chunk = blockIdx.x;
+  const int p0 = chunk * GN_CHUNK;
+  const int p1 = min(hw, p0 + GN_CHUNK);
+  const bf16* xi = x + (long)img * hw * ld;
+  const int cp = cs >> 3;
+  const int PL = 256 / cp;
+  const int t = threadIdx.x;
+  const int q = t % cp, pl = t / cp;
+  const bool active = pl < PL;
+  float s1[8], s2[8], K[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; K[e] = 0.f; }
+  if (active) {
+    bf16x8 k = *reinterpret_cast<const bf16x8*>(xi + q * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) K[e] = (float)k[e];
+    for (int p = p0 + pl; p < p1; p += PL) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(xi + (long)p * ld + q * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float d = (float)v[e] - K[e];
+        s1[e] += d;
+        s2[e] += d * d;
+      }
+    }
+  }
+  __shared__ float red[256 * 16];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[t * 16 + e] = s1[e]; red[t * 16 + 8 + e] = s2[e]; }
+  __syncthreads();
+  if (active && pl == 0) {
+    for (int l = 1; l < PL; ++l) {
+      const float* r = red + (l * cp + q) * 16;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] += r[e]; s2[e] += r[8 + e]; }
+    }
+    float* o = part + (((long)img * nchunk + chunk) * c + coff + q * 8) * 2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { o[2 * e] = s1[e]; o[2 * e + 1] = s2[e]; }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void gn_finalize_kernel(const T* __restrict__ x0, int c0, int ld0,
                                                          const T* __restrict__ x1, int ld1, int hw, int c, int groups,
@@ -117,20 +163,46 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const T* __restrict__ x
   }
 }
 
-// y = silu?(x*a + b) * out_mul, 8-wide when possible
+// y = silu?(x*a + b) * out_mul; ab rows have ab_c channels per image (ab points at channel 0 of x)
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, int n, int hw, int c, int ld,
-                                                       const float* __restrict__ ab, int silu, float out_mul,
-                                                       T* __restrict__ y, int yld) {
+                                                       const float* __restrict__ ab, int ab_c, int silu,
+                                                       float out_mul, T* __restrict__ y, int yld) {
   long total = (long)n * hw * c;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     long pix = i / c;
     int ch = (int)(i - pix * c);
     int img = (int)(pix / hw);
-    const float* p = ab + ((long)img * c + ch) * 2;
+    const float* p = ab + ((long)img * ab_c + ch) * 2;
     float v = to_f32(x[pix * ld + ch]) * p[0] + p[1];
     if (silu) v = silu_f(v);
     y[pix * yld + ch] = from_f32<T>(v * out_mul);
+  }
+}
+
+// 16-byte vectorised variant: one thread = 8 bf16 channels of one pixel (c, ld, yld multiples of 8)
+__global__ __launch_bounds__(256) void gn_apply_vec_kernel(const bf16* __restrict__ x, int n, int hw, int c, int ld,
+                                                           const float* __restrict__ ab, int ab_c, int silu,
+                                                           float out_mul, bf16* __restrict__ y, int yld) {
+  const int cp = c >> 3;
+  long total = (long)n * hw * cp;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    long pix = i / cp;
+    int ch = (int)(i - pix * cp) * 8;
+    int img = (int)(pix / hw);
+    const float4* p = reinterpret_cast<const float4*>(ab + ((long)img * ab_c + ch) * 2);
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(x + pix * ld + ch);
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 s = p[q];  // (a, b) of channels ch+2q, ch+2q+1
+      float v0 = (float)v[2 * q] * s.x + s.y;
+      float v1 = (float)v[2 * q + 1] * s.z + s.w;
+      if (silu) { v0 = silu_f(v0); v1 = silu_f(v1); }
+      o[2 * q] = (bf16)(v0 * out_mul);
+      o[2 * q + 1] = (bf16)(v1 * out_mul);
+    }
+    *reinterpret_cast<bf16x8*>(y + pix * yld + ch) = o;
   }
 }
 
@@ -165,11 +237,17 @@ int gn_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1
              int32_t groups, float eps, const float* gamma, const float* beta, float* ab, float* ws, hipStream_t s) {
   const int c = c0 + c1;
   const int nchunk = (hw + GN_CHUNK - 1) / GN_CHUNK;
-  hipLaunchKernelGGL(gn_partial_kernel<T>, dim3(nchunk, n), dim3(256), 0, s, (const T*)x0, hw, c0, ld0, 0, c, nchunk,
-                     ws);
-  if (c1 > 0)
-    hipLaunchKernelGGL(gn_partial_kernel<T>, dim3(nchunk, n), dim3(256), 0, s, (const T*)x1, hw, c1, ld1, c0, c,
-                       nchunk, ws);
+  auto seg = [&](const void* xs, int cs, int ld, int coff) {
+    const bool vec = sizeof(T) == 2 && cs % 8 == 0 && cs <= 2048 && ld % 8 == 0 && ((uintptr_t)xs) % 16 == 0;
+    if (vec)
+      hipLaunchKernelGGL(gn_partial_vec_kernel, dim3(nchunk, n), dim3(256), 0, s, (const bf16*)xs, hw, cs, ld, coff, c,
+                         nchunk, ws);
+    else
+      hipLaunchKernelGGL(gn_partial_kernel<T>, dim3(nchunk, n), dim3(256), 0, s, (const T*)xs, hw, cs, ld, coff, c,
+                         nchunk, ws);
+  };
+  seg(x0, c0, ld0, 0);
+  if (c1 > 0) seg(x1, c1, ld1, c0);
   hipLaunchKernelGGL(gn_finalize_kernel<T>, dim3(groups, n), dim3(64), 0, s, (const T*)x0, c0, ld0,
                      (const T*)(x1 ? x1 : x0), c1 > 0 ? ld1 : ld0, hw, c, groups, nchunk, ws, eps, gamma, beta, ab);
   return launch_status();
@@ -195,17 +273,25 @@ extern "C" int rdeic_groupnorm_stats(const void* x0, int32_t c0, int32_t ld0, co
 }
 
 extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32_t c, int32_t ld, const float* ab,
-                                     int32_t silu, float out_mul, void* y, int32_t yld, int32_t dtype, void* stream) {
-  if (!x || !ab || !y || n <= 0 || hw <= 0 || c <= 0) return RDEIC_EINVAL;
+                                     int32_t ab_c, int32_t silu, float out_mul, void* y, int32_t yld, int32_t dtype,
+                                     void* stream) {
+  if (!x || !ab || !y || n <= 0 || hw <= 0 || c <= 0 || ab_c < c) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   long total = (long)n * hw * c;
+  if (dtype == 1 && c % 8 == 0 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
+      ((uintptr_t)y) % 16 == 0 && ((uintptr_t)ab) % 16 == 0) {
+    int blocks = (int)std::min<long>((total / 8 + 255) / 256, 16384);
+    hipLaunchKernelGGL(gn_apply_vec_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld, ab, ab_c,
+                       silu, out_mul, (bf16*)y, yld);
+    return launch_status();
+  }
   int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   if (dtype == 1)
-    hipLaunchKernelGGL(gn_apply_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld, ab, silu,
-                       out_mul, (bf16*)y, yld);
+    hipLaunchKernelGGL(gn_apply_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld, ab, ab_c,
+                       silu, out_mul, (bf16*)y, yld);
   else
-    hipLaunchKernelGGL(gn_apply_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, n, hw, c, ld, ab, silu,
-                       out_mul, (float*)y, yld);
+    hipLaunchKernelGGL(gn_apply_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, n, hw, c, ld, ab, ab_c,
+                       silu, out_mul, (float*)y, yld);
   return launch_status();
 }
 

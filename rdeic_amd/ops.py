@@ -88,6 +88,15 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
            act: int = NONE, slope: float = 0.0, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False) -> torch.Tensor:
     """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC)."""
+    if gn is not None and _lds_dma_eligible(x, x2, p):
+        # the LDS-DMA conv path has no register stage to apply GroupNorm+SiLU in: materialise the
+        # normalised (concatenated) input once with the vectorised apply kernel instead
+        xin = torch.empty(x.shape[:3] + (p.cin,), dtype=x.dtype, device=x.device)
+        c0 = x.shape[3]
+        group_norm_apply(x, gn, gn_silu, out=xin[..., :c0])
+        if x2 is not None:
+            group_norm_apply(x2, gn[:, c0:], gn_silu, out=xin[..., c0:])
+        x, x2, gn = xin, None, None
     n, h, w, c0 = x.shape
     ld0 = pix_ld(x)
     c1, ld1 = 0, 0
@@ -147,8 +156,56 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     d.dtype = dt_code(x)
     d.out_f32 = int(odt == torch.float32 and x.dtype != torch.float32)
     d.batch = 1
-    call("rdeic_conv2d", C.byref(d), stream_ptr())
+    flops = 2.0 * n * ho * wo * p.cout * p.kh * p.kw * p.cin
+    prof = PROFILE
+    if prof is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        call("rdeic_conv2d", C.byref(d), stream_ptr())
+        ev1.record()
+        prof.append((flops, ev0, ev1, x.dtype))
+    else:
+        call("rdeic_conv2d", C.byref(d), stream_ptr())
     return out
+
+
+# When set to a list, every rdeic_conv2d launch appends (algorithmic FLOPs, start event, end
+# event, dtype) — bench.py uses it to time the dominant kernel live over its timed region.
+PROFILE = None
+
+
+def conv_profile_summary(records):
+    """(launches, total algorithmic FLOPs, total kernel ms) of recorded conv launches (after sync)."""
+    total_ms = 0.0
+    total_flops = 0.0
+    for flops, e0, e1, _ in records:
+        total_ms += e0.elapsed_time(e1)
+        total_flops += flops
+    return len(records), total_flops, total_ms
+
+
+CONV_PATH = 1  # mirrors rdeic_set_conv_path (1: LDS-DMA pipelined bf16 path)
+
+
+def set_conv_path(path: int) -> int:
+    global CONV_PATH
+    prev = CONV_PATH
+    CONV_PATH = int(path)
+    _lib.load().rdeic_set_conv_path(CONV_PATH)
+    return prev
+
+
+def _lds_dma_eligible(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) -> bool:
+    """Same rule as rdeic_conv2d's dispatch to conv_glds_kernel (bf16, 16-byte gathers, cout > 32)."""
+    if CONV_PATH == 0 or x.dtype != torch.bfloat16 or p.cout <= 32:
+        return False
+    for t in (x, x2):
+        if t is None:
+            continue
+        if t.shape[3] % 8 or t.stride(2) % 8 or t.data_ptr() % 16:
+            return False
+    return True
 
 
 def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[torch.Tensor] = None,
@@ -184,7 +241,16 @@ def gemm_batched(a: torch.Tensor, b_nk: torch.Tensor, out: torch.Tensor, *, batc
     d.out_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
     d.batch = batch
     d.in_bs, d.w_bs, d.out_bs = a_bs, b_bs, out_bs
-    call("rdeic_conv2d", C.byref(d), stream_ptr())
+    prof = PROFILE
+    if prof is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        call("rdeic_conv2d", C.byref(d), stream_ptr())
+        ev1.record()
+        prof.append((2.0 * batch * m * n * k, ev0, ev1, a.dtype))
+    else:
+        call("rdeic_conv2d", C.byref(d), stream_ptr())
     return out
 
 
@@ -204,11 +270,14 @@ def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, grou
 
 def group_norm_apply(x: torch.Tensor, ab: torch.Tensor, silu: bool, out: Optional[torch.Tensor] = None,
                      out_mul: float = 1.0) -> torch.Tensor:
+    """y = silu?(x*a + b) * out_mul; `ab` may be a channel slice ab[:, c0:] of a wider affine."""
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)
-    call("rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(), int(silu), float(out_mul),
-         out.data_ptr(), pix_ld(out), dt_code(x), stream_ptr())
+    if ab.shape[1] < c or ab.stride(2) != 1 or ab.stride(1) != 2:
+        raise ValueError("group-norm affine must be [n, >=c, 2] with packed (a, b) pairs")
+    call("rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(), ab.stride(0) // 2, int(silu),
+         float(out_mul), out.data_ptr(), pix_ld(out), dt_code(x), stream_ptr())
     return out
 
 
