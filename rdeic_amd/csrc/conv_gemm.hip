@@ -78,16 +78,19 @@ __device__ __forceinline__ uint4 gn_apply_chunk(uint4 raw, const float* ab, int 
   return *reinterpret_cast<uint4*>(v);
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, bool VEC>
-__global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
+// GNP: compile the GroupNorm+SiLU gather prologue in (false = plain gather, fewer VGPRs / VALU).
+template <typename T, int BM, int BN, int WGM, int WGN, bool VEC, bool GNP = true>
+__global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
+  constexpr int NT = WGM * WGN * 64;
   constexpr int BK = MmaTraits<T>::BK;
   constexpr int EPC = MmaTraits<T>::EPC;
   constexpr int ES = sizeof(T);
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int AR = BM / 32;                  // A chunks per thread (8 chunks per row, 256 threads)
-  constexpr int BR = (BN * 8 + 255) / 256;     // B chunks per thread
-  static_assert(TM >= 1 && TN >= 1, "tile");
+  constexpr int RPI = NT / 8;                  // tile rows covered per load instruction (8 chunks per row)
+  constexpr int AR = BM / RPI;                 // A chunks per thread
+  constexpr int BR = (BN + RPI - 1) / RPI;     // B chunks per thread
+  static_assert(TM >= 1 && TN >= 1 && AR >= 1 && BM % RPI == 0, "tile");
 
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // buffer b: A tile at lds + b*(BM+BN)*ROWB, B tile right after it
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
   int r_img[AR], r_iy[AR], r_ix[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
-    int m = m0 + (tid >> 3) + 32 * i;
+    int m = m0 + (tid >> 3) + RPI * i;
     if (m < a.M) {
       int img = m / hw_o, rem = m - img * hw_o;
       int oy = rem / a.wo, ox = rem - oy * a.wo;
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
               const T* src = (c < a.c0) ? reinterpret_cast<const T*>(a.in0) + pix * a.ld0 + c
                                         : reinterpret_cast<const T*>(a.in1) + pix * a.ld1 + (c - a.c0);
               x = to_f32(*src);
-              if (a.gn_ab) {
+              if (GNP && a.gn_ab) {
                 const float* ab = a.gn_ab + ((long)r_img[i] * a.cin + c) * 2;
                 x = x * ab[0] + ab[1];
                 if (a.gn_silu) x = silu_f(x);
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
   auto gather_b = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      int cid = tid + 256 * i;
+      int cid = tid + NT * i;
       int row = cid >> 3, ch = cid & 7;
       if (row < BN) {
         int nn = n0 + row;
@@ -204,15 +207,15 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
     for (int i = 0; i < AR; ++i) {
       uint4 v = areg[i];
       if constexpr (VEC) {
-        if (a.gn_ab && a_c[i] >= 0)
+        if (GNP && a.gn_ab && a_c[i] >= 0)
           v = gn_apply_chunk<T>(v, a.gn_ab + ((long)r_img[i] * a.cin + a_c[i]) * 2, a.gn_silu);
       }
-      int row = (tid >> 3) + 32 * i;
+      int row = (tid >> 3) + RPI * i;
       *reinterpret_cast<uint4*>(AS(buf) + row * ROWB + kc * 16) = v;
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      int cid = tid + 256 * i;
+      int cid = tid + NT * i;
       int row = cid >> 3, ch = cid & 7;
       if (row < BN) *reinterpret_cast<uint4*>(BS(buf) + row * ROWB + ch * 16) = breg[i];
     }
@@ -239,16 +242,30 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a) {
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8 af[TM], bfv[TN];
+        if constexpr (TM * TN > 16) {
+          // big wave tiles: hold the B fragments, stream A fragments one at a time (register budget)
+          bf16x8 bfv[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROWB + s * 64 + lq * 16);
+          for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROWB + s * 64 + lq * 16);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROWB + s * 64 + lq * 16);
+          for (int i = 0; i < TM; ++i) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROWB + s * 64 + lq * 16);
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+          }
+        } else {
+          bf16x8 af[TM], bfv[TN];
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROWB + s * 64 + lq * 16);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROWB + s * 64 + lq * 16);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+        }
       }
     } else {
 #pragma unroll
@@ -319,10 +336,45 @@ int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
   dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
   size_t lds = 2 * (BM + BN) * ROWB;
   if (vec)
-    hipLaunchKernelGGL((conv_kernel<T, BM, BN, WGM, WGN, true>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((conv_kernel<T, BM, BN, WGM, WGN, true>), grid, dim3(WGM * WGN * 64), lds, s, a);
   else
-    hipLaunchKernelGGL((conv_kernel<T, BM, BN, WGM, WGN, false>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((conv_kernel<T, BM, BN, WGM, WGN, false>), grid, dim3(WGM * WGN * 64), lds, s, a);
   return launch_status();
+}
+
+// register-staged, no GN prologue (bf16, 16-byte gathers): the big-tile main path
+template <int BM, int BN, int WGM, int WGN>
+int launch_plain(const ConvArgs& a, hipStream_t s) {
+  dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
+  size_t lds = 2 * (BM + BN) * ROWB;
+  hipLaunchKernelGGL((conv_kernel<bf16, BM, BN, WGM, WGN, true, false>), grid, dim3(WGM * WGN * 64), lds, s, a);
+  return launch_status();
+}
+
+// Tile choice for the plain path: maximise (useful fraction of the padded tile grid) x (CU fill)
+// x (operand reuse of the tile); the accumulation order does not depend on the choice.
+int launch_plain_auto(const ConvArgs& a, hipStream_t s) {
+  struct Cand { int bm, bn; float reuse; };
+  const Cand cands[] = {{256, 256, 1.0f}, {256, 128, 0.86f}, {128, 256, 0.86f}, {128, 128, 0.72f}, {64, 128, 0.55f},
+                        {128, 64, 0.55f}};
+  int best = 3;
+  float best_score = -1.f;
+  for (int i = 0; i < 6; ++i) {
+    const long tm = cdiv(a.M, cands[i].bm), tn = cdiv(a.cout, cands[i].bn);
+    const float useful = (float)a.M * a.cout / ((float)tm * cands[i].bm * tn * cands[i].bn);
+    const float blocks = (float)tm * tn * a.batch;
+    const float fill = blocks >= 256.f ? 1.f : blocks / 256.f;
+    const float score = useful * fill * cands[i].reuse;
+    if (score > best_score + 1e-6f) { best_score = score; best = i; }
+  }
+  switch (best) {
+    case 0: return launch_plain<256, 256, 4, 4>(a, s);
+    case 1: return launch_plain<256, 128, 4, 2>(a, s);
+    case 2: return launch_plain<128, 256, 2, 4>(a, s);
+    case 3: return launch_plain<128, 128, 2, 2>(a, s);
+    case 4: return launch_plain<64, 128, 2, 2>(a, s);
+    default: return launch_plain<128, 64, 2, 2>(a, s);
+  }
 }
 
 // ============================================================================================
@@ -336,7 +388,7 @@ int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
 // No GroupNorm prologue here: GN+SiLU inputs are materialised by rdeic_groupnorm_apply first.
 // ============================================================================================
 __device__ uint4 g_zero_page[64];  // 1 KiB of zeros: source of every padded / out-of-range chunk
-int g_conv_path = 1;
+int g_conv_path = 2;  // 0: register-staged + fused GN, 1: LDS-DMA ring, 2: register-staged big tiles
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -553,12 +605,13 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
   if (d->c1) vec = vec && (d->c1 % epc == 0) && (d->ld1 % epc == 0) && (((uintptr_t)d->in1) % 16 == 0);
   if (((uintptr_t)d->weight) % 16 != 0) return RDEIC_EINVAL;
 
-  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path != 0) {
+  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 1) {
     // LDS-DMA pipelined path (wld % 64 == 0 and 16-byte aligned rows are guaranteed above)
     if (d->cout % 128 != 0 && d->cout % 64 == 0) return launch_glds<128, 64, 2, 2, 3>(a, s);
     if (a.M <= 8192) return launch_glds<64, 128, 2, 2, 3>(a, s);
     return launch_glds<128, 128, 2, 2, 3>(a, s);
   }
+  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 2) return launch_plain_auto(a, s);
   if (d->dtype == 1) {
     if (d->cout <= 16) return launch_cfg<bf16, 128, 16, 4, 1>(a, vec, s);
     if (d->cout <= 32) return launch_cfg<bf16, 128, 32, 4, 1>(a, vec, s);

@@ -164,7 +164,8 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
         ev0.record()
         call("rdeic_conv2d", C.byref(d), stream_ptr())
         ev1.record()
-        prof.append((flops, ev0, ev1, x.dtype))
+        prof.append((flops, ev0, ev1, x.dtype,
+                     (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), int(pixel_shuffle))))
     else:
         call("rdeic_conv2d", C.byref(d), stream_ptr())
     return out
@@ -179,13 +180,27 @@ def conv_profile_summary(records):
     """(launches, total algorithmic FLOPs, total kernel ms) of recorded conv launches (after sync)."""
     total_ms = 0.0
     total_flops = 0.0
-    for flops, e0, e1, _ in records:
+    for rec in records:
+        flops, e0, e1 = rec[0], rec[1], rec[2]
         total_ms += e0.elapsed_time(e1)
         total_flops += flops
     return len(records), total_flops, total_ms
 
 
-CONV_PATH = 1  # mirrors rdeic_set_conv_path (1: LDS-DMA pipelined bf16 path)
+def conv_profile_breakdown(records):
+    """{shape-class: [launches, GFLOP, ms]} for diagnosing where the conv time goes."""
+    out = {}
+    for rec in records:
+        flops, e0, e1, meta = rec[0], rec[1], rec[2], rec[4]
+        key = str(meta)
+        v = out.setdefault(key, [0, 0.0, 0.0])
+        v[0] += 1
+        v[1] += flops / 1e9
+        v[2] += e0.elapsed_time(e1)
+    return out
+
+
+CONV_PATH = 2  # mirrors rdeic_set_conv_path (0 fused-GN 128-tiles, 1 LDS-DMA ring, 2 big register-staged tiles)
 
 
 def set_conv_path(path: int) -> int:
@@ -248,7 +263,7 @@ def gemm_batched(a: torch.Tensor, b_nk: torch.Tensor, out: torch.Tensor, *, batc
         ev0.record()
         call("rdeic_conv2d", C.byref(d), stream_ptr())
         ev1.record()
-        prof.append((2.0 * batch * m * n * k, ev0, ev1, a.dtype))
+        prof.append((2.0 * batch * m * n * k, ev0, ev1, a.dtype, ("bgemm", batch, m, n, k)))
     else:
         call("rdeic_conv2d", C.byref(d), stream_ptr())
     return out

@@ -1,0 +1,74 @@
+"""Conv kernel micro-benchmark on the hot path's conv shapes (bf16, batch 16 @ 512x512 images).
+Interleaves the register-staged (path 0) and LDS-DMA (path 1) kernels in one process and
+checks that both produce bit-identical outputs (same k-order, same MFMA)."""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rdeic_amd import ops  # noqa: E402
+
+SHAPES = [  # (name, B, H, W, cin, cout, k, stride)
+    ("unet320@64", 16, 64, 64, 320, 320, 3, 1),
+    ("unet640@32", 16, 32, 32, 640, 640, 3, 1),
+    ("unet1280@16", 16, 16, 16, 1280, 1280, 3, 1),
+    ("unet1280@8", 16, 8, 8, 1280, 1280, 3, 1),
+    ("unet_cat2560@8", 16, 8, 8, 2560, 1280, 3, 1),
+    ("vae128@512", 16, 512, 512, 128, 128, 3, 1),
+    ("vae256@256", 16, 256, 256, 256, 256, 3, 1),
+    ("vae512@128", 16, 128, 128, 512, 512, 3, 1),
+    ("vae512@64", 16, 64, 64, 512, 512, 3, 1),
+    ("linear320x1280 (ff)", 16, 64, 64, 320, 2560, 1, 1),
+]
+
+
+def bench(fn, reps):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--paths", default="0,1,2")
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    res = []
+    for name, B, H, W, cin, cout, k, stride in SHAPES:
+        if args.only and args.only not in name:
+            continue
+        x = torch.randn(B, H, W, cin, device="cuda").to(torch.bfloat16)
+        w = torch.randn(cout, cin, k, k, device="cuda") / math.sqrt(cin * k * k)
+        p = ops.ConvParams.pack(w, torch.randn(cout, device="cuda"), stride=stride, pad=k // 2)
+        paths = [int(v) for v in args.paths.split(",")]
+        outs = {}
+        times = {q: [] for q in paths}
+        for path in paths:
+            ops.set_conv_path(path)
+            outs[path] = ops.conv2d(x, p)
+        for _ in range(3):
+            for path in paths:
+                ops.set_conv_path(path)
+                times[path].append(bench(lambda: ops.conv2d(x, p), args.reps))
+        flops = 2.0 * B * (H // stride) * (W // stride) * cout * cin * k * k
+        r = dict(name=name)
+        for q in paths:
+            r[f"tflops_p{q}"] = round(flops / min(times[q]) / 1e12, 1)
+        r["identical"] = all(torch.equal(outs[paths[0]], outs[q]) for q in paths)
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    ops.set_conv_path(2)
+
+
+if __name__ == "__main__":
+    main()
