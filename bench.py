@@ -107,7 +107,7 @@ def main():
     if not args.no_cpu_baseline:
         try:
             from oracle.bench_cpu import run_cpu_baseline
-            cpu = run_cpu_baseline(size=S, ddim_steps=args.ddim_steps)
+            cpu = run_cpu_baseline(size=S, steps=args.ddim_steps)
         except Exception as e:  # the baseline is reported, never the target
             cpu = {"value": None, "error": f"{type(e).__name__}: {e}"}
     line = {

@@ -1,0 +1,43 @@
+"""ORACLE / TEST INFRASTRUCTURE: the `cpu_baseline` leg of bench.py.
+
+Times the oracle restatement (fp32 torch on the host cores, C rANS twin, pure-Python torchac
+twin for the 4x4..(H/128)^2 hyper-latent) on a bounded sample of the bench workload: `n_images`
+images of the same size/steps, one at a time as reference inference.py:83-147 processes them.
+"""
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import model_ref as M
+
+
+def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads: int = None):
+    from rdeic_amd.synthetic import sampler_noise, synth_context, synth_image  # test-input generators
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        sd = M.synthetic_state_dict()
+        tables = M.Tables()
+        ctx = synth_context()
+        imgs = [synth_image(size, size, 231 + i) for i in range(n_images)]
+        noises = [sampler_noise((1, 4, size // 8, size // 8), 231 + i)[1] for i in range(n_images)]
+        with torch.no_grad():
+            t0 = time.perf_counter()
+            for img, nz in zip(imgs, noises):
+                M.codec_image(sd, tables, img, ctx, nz, steps=steps, coder="c")
+            dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(n_images / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n_images} image(s) {size}x{size}, {steps} DDIM steps, full encode->code->"
+                      f"relay->decode on torch-CPU fp32 ({dt:.1f} s)"}
+
+
+if __name__ == "__main__":
+    import json
+    import sys
+    print(json.dumps(run_cpu_baseline(size=int(sys.argv[1]) if len(sys.argv) > 1 else 512)))
