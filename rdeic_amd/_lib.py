@@ -61,6 +61,7 @@ PROTOTYPES = {
                                         _i32, _p]),
     "rdeic_groupnorm_apply": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _i32, _f, _p, _i32, _i32, _p]),
     "rdeic_set_conv_path": (C.c_int, [_i32]),
+    "rdeic_set_conv_option": (C.c_int, [_i32, _i32]),
     "rdeic_layernorm": (C.c_int, [_p, _i32, _i32, _i32, _p, _p, _f, _p, _i32, _i32, _p]),
     "rdeic_softmax_rows": (C.c_int, [_p, _i64, _i32, _f, _p, _i32, _p]),
     "rdeic_transpose": (C.c_int, [_p, _i32, _i32, _i32, _p, _i32, _i32, _i64, _i64, _i32, _p]),

@@ -39,6 +39,7 @@ struct ConvArgs {
   int M, cin, ktot, nk;
   long in_bs, w_bs, out_bs;  // batched-GEMM strides (elements), blockIdx.z
   int batch;
+  int epi_vec;               // 1: LDS-staged vector epilogue where eligible
 };
 
 constexpr int ROWB = 144;  // LDS bytes per tile row: 128 B of k-data + 16 B pad (bank spread)
@@ -76,6 +77,92 @@ __device__ __forceinline__ uint4 gn_apply_chunk(uint4 raw, const float* ab, int 
     v[e] = from_f32<T>(x);
   }
   return *reinterpret_cast<uint4*>(v);
+}
+
+// Vectorised epilogue through LDS (bf16 activations; out_mode 0): the accumulators of half the
+// tile rows at a time are parked in LDS as fp32, then re-read row-contiguous 8 at a time so the
+// bias / emb / activation / residual are applied per 8-wide chunk and the residual load and the
+// output store are 16-byte coalesced vectors. Same fp32 operation order as the scalar epilogue
+// ((acc + bias) + emb -> act -> + res -> round), so results are bit-identical to it.
+// Needs BM/2 * (BN + 4) * 4 bytes of LDS; the caller has finished with its k-loop buffers.
+__device__ __forceinline__ bool epi_vec_ok(const ConvArgs& a) {
+  const bool of32 = a.out_f32;
+  return a.out_mode == 0 && (a.cout % 8) == 0 && (a.out_ld % 8) == 0 && ((uintptr_t)a.out % 16) == 0 &&
+         (!a.res || ((a.res_ld % 8) == 0 && ((uintptr_t)a.res % 16) == 0)) && (!of32 || true);
+}
+
+template <int BM, int BN, int WGM, int WGN, int NT>
+__device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16], const ConvArgs& a,
+                                             int m0, int n0, int wm, int wn, int lane, int tid, char* lds) {
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int HM = TM / 2;                    // fragment rows per pass
+  constexpr int PR = BM / 2;                    // tile rows per pass
+  constexpr int SDW = BN + 4;                   // LDS row stride in dwords (bank spread)
+  constexpr int CPR = BN / 8;                   // 8-wide chunks per row
+  static_assert(TM % 2 == 0, "two passes");
+  const int lr = lane & 15, lq = lane >> 4;
+  float* L = reinterpret_cast<float*>(lds);
+  const int hw_o = a.ho * a.wo;
+  const bool of32 = a.out_f32;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    __syncthreads();
+#pragma unroll
+    for (int ii = 0; ii < HM; ++ii)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pr = wm * (WTM / 2) + ii * 16 + lq * 4 + r;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) L[pr * SDW + wn * WTN + j * 16 + lr] = acc[p * HM + ii][j][r];
+      }
+    __syncthreads();
+    for (int c = tid; c < PR * CPR; c += NT) {
+      const int pr = c / CPR, cc = c - pr * CPR;
+      // pass-local row pr -> wave row block wm' = pr / (WTM/2), row within = pr % (WTM/2)
+      const int wmr = pr / (WTM / 2), wr = pr - wmr * (WTM / 2);
+      const int m = m0 + wmr * WTM + p * (WTM / 2) + wr;
+      const int nn = n0 + cc * 8;
+      if (m >= a.M || nn >= a.cout) continue;
+      float v[8];
+      const float4 x0 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8 + 4);
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      if (a.bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += a.bias[nn + e];
+      }
+      if (a.emb) {
+        const float* em = a.emb + (long)(m / hw_o) * a.emb_ld + nn;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += em[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act, a.act_param);
+      if (a.res) {
+        if (of32) {
+          const float4 r0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.res) + (long)m * a.res_ld + nn);
+          const float4 r1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.res) + (long)m * a.res_ld + nn + 4);
+          v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+        } else {
+          bf16 rv[8];
+          *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.res) + (long)m * a.res_ld + nn);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += to_f32(rv[e]);
+        }
+      }
+      if (of32) {
+        float* o = reinterpret_cast<float*>(a.out) + (long)m * a.out_ld + nn;
+        *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        bf16 ov[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[e] = from_f32<bf16>(v[e]);
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + nn) = *reinterpret_cast<uint4*>(ov);
+      }
+    }
+  }
 }
 
 // GNP: compile the GroupNorm+SiLU gather prologue in (false = plain gather, fewer VGPRs / VALU).
@@ -288,6 +375,12 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 
 #undef AS
 #undef BS
+  if constexpr (sizeof(T) == 2 && TM % 2 == 0 && (BM / 2) * (BN + 4) * 4 <= 2 * (BM + BN) * ROWB) {
+    if (a.epi_vec && epi_vec_ok(a)) {
+      epilogue_vec<BM, BN, WGM, WGN, NT>(acc, a, m0, n0, wm, wn, lane, tid, lds);
+      return;
+    }
+  }
   // ---------------- epilogue: C[m][n], lane holds col n = lane&15, rows 4*lq + r
   const bool of32 = (sizeof(T) == 4) || a.out_f32;
 #pragma unroll
@@ -389,6 +482,7 @@ int launch_plain_auto(const ConvArgs& a, hipStream_t s) {
 // ============================================================================================
 __device__ uint4 g_zero_page[64];  // 1 KiB of zeros: source of every padded / out-of-range chunk
 int g_conv_path = 2;  // 0: register-staged + fused GN, 1: LDS-DMA ring, 2: register-staged big tiles
+int g_epi_vec = 1;    // LDS-staged vector epilogue (rdeic_set_conv_option(0, v))
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -524,6 +618,13 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_glds_kernel(ConvArgs a) {
   }
 
   // ---------------- epilogue (same semantics as conv_kernel)
+  if constexpr ((BM / 2) * (BN + 4) * 4 <= STAGES * STAGE) {
+    if (a.epi_vec && epi_vec_ok(a)) {
+      __syncthreads();  // every wave is past its last ds_read of the ring
+      epilogue_vec<BM, BN, WGM, WGN, 512>(acc, a, m0, n0, wm, wn, lane, tid, lds);
+      return;
+    }
+  }
   const bool of32 = a.out_f32;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -568,6 +669,217 @@ int launch_glds(const ConvArgs& a, hipStream_t s) {
   return launch_status();
 }
 
+// ============================================================================================
+// bf16 path 3: one workgroup per CU, 8 waves, big tiles (256x256: 2x4 waves of 128x64;
+// 512x128: 4x2 waves of 128x64), BK = 32 (64-byte LDS rows), STAGES-deep LDS-DMA ring for BOTH
+// operands with a counted vmcnt (loads stay in flight across the raw s_barrier; the loop never
+// drains to 0), one barrier per k-step. LDS rows are 64 B = 4 chunks of 16 B; chunk c of row r
+// lives in slot c ^ key(r), key(r) = bit1(r) | bit2(r) << 1, which makes every ds_read_b128
+// lane group of the 16x16x32 fragment read cover all 64 banks exactly once. Since rows handled
+// by one lane differ by multiples of 16, the key is a per-lane constant on both the DMA side
+// (source pre-swizzle) and the read side. Blocks are remapped so each XCD owns a contiguous run
+// of tiles (N fastest): neighbouring M tiles share input halo rows and all N tiles share the A
+// panel in that XCD's L2. The K order is the same as every other path (k ascending, one
+// 16x16x32 MFMA per 32-k step), so results are bit-identical to paths 0-2.
+// ============================================================================================
+__device__ __forceinline__ int ring_key(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1); }
+
+template <int BM, int BN, int WGM, int WGN, int STAGES>
+__global__ __launch_bounds__(512) void conv_ring_kernel(ConvArgs a, int tiles_m, int tiles_n) {
+  constexpr int NW = 8;
+  static_assert(WGM * WGN == NW, "8 waves");
+  constexpr int ROW = 64;                       // bytes per LDS row (32 bf16 of k)
+  constexpr int A_BYTES = BM * ROW, STAGE = (BM + BN) * ROW;
+  constexpr int AI = BM / 128, BI = BN / 128;   // glds per lane per stage (16 rows x 64 B per wave-instr)
+  constexpr int PER = AI + BI;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(AI >= 1 && BI >= 1 && AI * 128 == BM && BI * 128 == BN, "tile");
+  static_assert(STAGES >= 3 && STAGES <= 5, "stages");
+
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  // XCD-aware bijective remap of the 1-D grid (blocks with equal orig % 8 share an XCD)
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+  const int per_z = tiles_m * tiles_n;
+  const int bz = wgid / per_z;
+  const int rem_t = wgid - bz * per_z;
+  const int tile_m = rem_t / tiles_n, tile_n = rem_t - tile_m * tiles_n;
+  if (bz > 0) {
+    a.in0 += (long)bz * a.in_bs * 2; a.in1 += (long)bz * a.in_bs * 2;
+    a.weight += (long)bz * a.w_bs * 2;
+    a.out += (long)bz * a.out_bs * (a.out_f32 ? 4 : 2);
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int hw_o = a.ho * a.wo;
+  const int hin = a.up2 ? 2 * a.h : a.h, win = a.up2 ? 2 * a.w : a.w;
+  const int lrow = lane >> 2;                          // row within this wave-instruction's 16 rows
+  const int g = (lane & 3) ^ ring_key(lrow);           // k-chunk this lane stages (fixed)
+  const char* zp = reinterpret_cast<const char*>(g_zero_page);
+
+  int r_img[AI], r_iy[AI], r_ix[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int m = m0 + 16 * (j * NW + wave) + lrow;
+    if (m < a.M) {
+      int img = m / hw_o, rem = m - img * hw_o;
+      int oy = rem / a.wo, ox = rem - oy * a.wo;
+      r_img[j] = img;
+      r_iy[j] = oy * a.stride - a.pad_t;
+      r_ix[j] = ox * a.stride - a.pad_l;
+    } else {
+      r_img[j] = -1; r_iy[j] = 0; r_ix[j] = 0;
+    }
+  }
+  const char* b_row[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int nn = n0 + 16 * (j * NW + wave) + lrow;
+    b_row[j] = nn < a.cout ? a.weight + ((long)nn * a.wld + g * 8) * 2 : nullptr;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    char* sb = lds + buf * STAGE;
+    const int k0 = kt * 32 + g * 8;
+    const bool kval = k0 < a.ktot;
+    const int tap = kval ? k0 / a.cin : 0;
+    const int c = k0 - tap * a.cin;
+    const int ky = tap / a.kw, kx = tap - ky * a.kw;
+    const char* base; int ld, cs;
+    if (c < a.c0) { base = a.in0; ld = a.ld0; cs = c; } else { base = a.in1; ld = a.ld1; cs = c - a.c0; }
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      int iy = r_iy[j] + ky, ix = r_ix[j] + kx;
+      const bool ok = kval && r_img[j] >= 0 && iy >= 0 && iy < hin && ix >= 0 && ix < win;
+      if (a.up2) { iy >>= 1; ix >>= 1; }
+      const char* src = ok ? base + ((((long)r_img[j] * a.h + iy) * a.w + ix) * ld + cs) * 2 : zp;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(sb + 16 * (j * NW + wave) * ROW),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const char* src = b_row[j] ? b_row[j] + (long)kt * 64 : zp;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src, (__attribute__((address_space(3))) void*)(sb + A_BYTES + 16 * (j * NW + wave) * ROW),
+          16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lq = lane >> 4;
+  const int slot = (lq ^ ring_key(lr)) * 16;
+  const int nk = (a.ktot + 31) / 32;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int after = min(STAGES - 2, nk - 1 - kt);  // stages issued after tile kt so far
+    if constexpr (STAGES == 5) {
+      if (after >= 3) wait_vmcnt<3 * PER>();
+      else if (after == 2) wait_vmcnt<2 * PER>();
+      else if (after == 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+    } else if constexpr (STAGES == 4) {
+      if (after >= 2) wait_vmcnt<2 * PER>();
+      else if (after == 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+    } else {
+      if (after >= 1) wait_vmcnt<PER>();
+      else wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* sb = lds + (kt % STAGES) * STAGE;
+    const char* Ab = sb + (wm * WTM + lr) * ROW + slot;
+    const char* Bb = sb + A_BYTES + (wn * WTN + lr) * ROW + slot;
+    bf16x8 bfv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROW);
+    bf16x8 af[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROW);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
+  // ---------------- epilogue (same semantics as conv_kernel)
+  const bool of32 = a.out_f32;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
+      if (m >= a.M) continue;
+      const int img = m / hw_o;
+      int oy = 0, ox = 0;
+      if (a.out_mode == 1) { int rem = m - img * hw_o; oy = rem / a.wo; ox = rem - oy * a.wo; }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nn = n0 + wn * WTN + j * 16 + lr;
+        if (nn >= a.cout) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v += a.bias[nn];
+        if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
+        v = apply_act(v, a.act, a.act_param);
+        long oidx, ridx;
+        if (a.out_mode == 1) {
+          int c = nn >> 2, dy = (nn >> 1) & 1, dx = nn & 1;
+          long p = ((long)img * (2 * a.ho) + (2 * oy + dy)) * (2 * a.wo) + (2 * ox + dx);
+          oidx = p * a.out_ld + c;
+          ridx = p * a.res_ld + c;
+        } else {
+          oidx = (long)m * a.out_ld + nn;
+          ridx = (long)m * a.res_ld + nn;
+        }
+        if (a.res) v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const bf16*>(a.res)[ridx]);
+        if (of32) reinterpret_cast<float*>(a.out)[oidx] = v;
+        else reinterpret_cast<bf16*>(a.out)[oidx] = from_f32<bf16>(v);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int STAGES>
+int launch_ring(const ConvArgs& a, hipStream_t s) {
+  const int tm = cdiv(a.M, BM), tn = cdiv(a.cout, BN);
+  const long nwg = (long)tm * tn * a.batch;
+  if (nwg > 0x7fffffffL) return RDEIC_EINVAL;
+  const size_t lds = (size_t)STAGES * (BM + BN) * 64;
+  hipLaunchKernelGGL((conv_ring_kernel<BM, BN, WGM, WGN, STAGES>), dim3((unsigned)nwg), dim3(512), lds, s, a, tm, tn);
+  return launch_status();
+}
+
+// Path 3 tile choice: 256x256 unless cout <= 128 (then 512x128); returns -1 when the shape is
+// better served by the smaller tiles of path 2 (too few tiles to fill the chip).
+int launch_ring_auto(const ConvArgs& a, hipStream_t s) {
+  const long t256 = (long)cdiv(a.M, 256) * cdiv(a.cout, 256) * a.batch;
+  const long t512 = (long)cdiv(a.M, 512) * cdiv(a.cout, 128) * a.batch;
+  const float u256 = (float)a.cout / (cdiv(a.cout, 256) * 256.f);
+  const float u128 = (float)a.cout / (cdiv(a.cout, 128) * 128.f);
+  if (u128 > u256 + 0.01f && t512 >= 256) return launch_ring<512, 128, 4, 2, 4>(a, s);
+  if (t256 >= 256) return launch_ring<256, 256, 2, 4, 4>(a, s);
+  return -1;
+}
+
 }  // namespace
 
 extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
@@ -589,6 +901,7 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
   a.res = (const char*)d->res; a.res_ld = d->res_ld;
   a.out = (char*)d->out; a.out_ld = d->out_ld; a.out_mode = d->out_mode;
   a.out_f32 = d->out_f32;
+  a.epi_vec = g_epi_vec;
   a.M = d->n * d->ho * d->wo;
   a.batch = d->batch > 1 ? d->batch : 1;
   a.in_bs = d->in_bs; a.w_bs = d->w_bs; a.out_bs = d->out_bs;
@@ -611,6 +924,11 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
     if (a.M <= 8192) return launch_glds<64, 128, 2, 2, 3>(a, s);
     return launch_glds<128, 128, 2, 2, 3>(a, s);
   }
+  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 3) {
+    const int rc = launch_ring_auto(a, s);
+    if (rc != -1) return rc;
+    return launch_plain_auto(a, s);
+  }
   if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 2) return launch_plain_auto(a, s);
   if (d->dtype == 1) {
     if (d->cout <= 16) return launch_cfg<bf16, 128, 16, 4, 1>(a, vec, s);
@@ -628,4 +946,9 @@ extern "C" int rdeic_set_conv_path(int32_t path) {
   int prev = g_conv_path;
   g_conv_path = path;
   return prev;
+}
+
+extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
+  if (key == 0) { int prev = g_epi_vec; g_epi_vec = value; return prev; }
+  return RDEIC_EINVAL;
 }

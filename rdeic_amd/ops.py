@@ -211,6 +211,11 @@ def set_conv_path(path: int) -> int:
     return prev
 
 
+def set_conv_option(key: int, value: int) -> int:
+    """rdeic_set_conv_option: key 0 = vectorised LDS-staged epilogue (1 on, 0 off)."""
+    return int(_lib.load().rdeic_set_conv_option(int(key), int(value)))
+
+
 def _lds_dma_eligible(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) -> bool:
     """Same rule as rdeic_conv2d's dispatch to conv_glds_kernel (bf16, 16-byte gathers, cout > 32)."""
     if CONV_PATH == 0 or x.dtype != torch.bfloat16 or p.cout <= 32:

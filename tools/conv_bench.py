@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--paths", default="0,1,2")
+    ap.add_argument("--epi", default="1", help="comma list of epilogue modes to A/B (1 vector, 0 scalar)")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []
@@ -50,24 +51,29 @@ def main():
         x = torch.randn(B, H, W, cin, device="cuda").to(torch.bfloat16)
         w = torch.randn(cout, cin, k, k, device="cuda") / math.sqrt(cin * k * k)
         p = ops.ConvParams.pack(w, torch.randn(cout, device="cuda"), stride=stride, pad=k // 2)
-        paths = [int(v) for v in args.paths.split(",")]
+        res_t = torch.randn(B, H // stride, W // stride, cout, device="cuda").to(torch.bfloat16)
+        paths = [(int(v), int(e)) for v in args.paths.split(",") for e in args.epi.split(",")]
         outs = {}
         times = {q: [] for q in paths}
-        for path in paths:
+        fn = lambda: ops.conv2d(x, p, res=res_t, act=ops.SILU)  # noqa: E731
+        for path, epi in paths:
             ops.set_conv_path(path)
-            outs[path] = ops.conv2d(x, p)
+            ops.set_conv_option(0, epi)
+            outs[(path, epi)] = fn()
         for _ in range(3):
-            for path in paths:
+            for path, epi in paths:
                 ops.set_conv_path(path)
-                times[path].append(bench(lambda: ops.conv2d(x, p), args.reps))
+                ops.set_conv_option(0, epi)
+                times[(path, epi)].append(bench(fn, args.reps))
         flops = 2.0 * B * (H // stride) * (W // stride) * cout * cin * k * k
         r = dict(name=name)
         for q in paths:
-            r[f"tflops_p{q}"] = round(flops / min(times[q]) / 1e12, 1)
+            r[f"tflops_p{q[0]}e{q[1]}"] = round(flops / min(times[q]) / 1e12, 1)
         r["identical"] = all(torch.equal(outs[paths[0]], outs[q]) for q in paths)
         print(json.dumps(r), flush=True)
         res.append(r)
     ops.set_conv_path(2)
+    ops.set_conv_option(0, 1)
 
 
 if __name__ == "__main__":
