@@ -167,6 +167,15 @@ class Compression:
         return zq
 
     # ------------------------------------------------------------------ entropy stages
+    def _pinned(self, key: str, n: int, dtype=torch.int32) -> torch.Tensor:
+        """Reusable page-locked host staging buffer (>= n elements) for the coder round trips."""
+        cache = self.__dict__.setdefault("_pin_cache", {})
+        buf = cache.get(key)
+        if buf is None or buf.numel() < n or buf.dtype != dtype:
+            buf = torch.empty(max(n, 1), dtype=dtype, pin_memory=True)
+            cache[key] = buf
+        return buf[:n]
+
     def stage_sizes(self, hy: int, wy: int) -> List[int]:
         sizes = []
         for c in self.slice_ch:
@@ -232,7 +241,12 @@ class Compression:
                      ops.stream_ptr())
 
         self._run_stages(hyper, B, hy, wy, emit)
-        sym_h, idx_h, zi = sym.cpu().numpy(), idx.cpu().numpy(), z_idx.cpu().numpy()
+        sym_p = self._pinned("enc_sym", B * total).view(B, total)
+        idx_p = self._pinned("enc_idx", B * total).view(B, total)
+        sym_p.copy_(sym, non_blocking=True)
+        idx_p.copy_(idx, non_blocking=True)
+        zi = z_idx.cpu().numpy()  # synchronises the stream: the pinned copies above are complete
+        sym_h, idx_h = sym_p.numpy(), idx_p.numpy()
         y_strings = coders.rans_encode_batch(sym_h, idx_h, self.tables)
         hz, wz = z.shape[1], z.shape[2]
         out = []
@@ -255,6 +269,8 @@ class Compression:
         hyper = self._seq(self.hyper_dec, z_q)
         _, hy, wy, _ = hyper.shape
         decs = [coders.RansDecoder(st[0][0]) for st in strings_list]
+        nmax = B * max(self.stage_sizes(hy, wy))
+        self._pinned("dec_idx", nmax), self._pinned("dec_sym", nmax)  # size once: no regrowth mid-loop
         table = self.tables.device_scale_table(hyper.device)
         dtc = ops.dt_code(hyper)
 
@@ -264,8 +280,12 @@ class Compression:
             ops.call("rdeic_ckbd_indexes", params.data_ptr(), ops.pix_ld(params), B, hy, wy, c, phase,
                      table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), idx.data_ptr(), n, 0, dtc,
                      ops.stream_ptr())
-            sym_h = coders.rans_decode_batch(decs, idx.cpu().numpy(), self.tables)
-            sym = torch.from_numpy(sym_h).to(hyper.device)
+            idx_p = self._pinned("dec_idx", B * n).view(B, n)
+            idx_p.copy_(idx, non_blocking=True)
+            torch.cuda.current_stream(hyper.device).synchronize()
+            sym_p = self._pinned("dec_sym", B * n).view(B, n)
+            coders.rans_decode_batch(decs, idx_p.numpy(), self.tables, out=sym_p.numpy())
+            sym = sym_p.to(hyper.device, non_blocking=True)
             ops.call("rdeic_ckbd_dequant", sym.data_ptr(), params.data_ptr(), ops.pix_ld(params), B, hy, wy, c, phase,
                      n, 0, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
                      None if anchor is None else anchor.data_ptr(), 0 if anchor is None else ops.pix_ld(anchor), dtc,

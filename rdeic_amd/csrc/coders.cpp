@@ -19,6 +19,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cmath>
 #include <new>
 #include <thread>
@@ -189,25 +192,79 @@ int rans_decode_impl(RansDecoder* d, const int32_t* idx, size_t n, const int32_t
   return d->bad ? RDEIC_EBADMSG : RDEIC_OK;
 }
 
+// Persistent host worker pool: the decoder is called once per checkerboard stage (20x per
+// batch), so spawning threads per call would cost more than the decode of a small stage.
+// One job runs at a time (callers serialise on job_mu); the caller thread works too.
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool* p = new WorkerPool();  // intentionally leaked: workers outlive static dtors
+    return *p;
+  }
+  void run(int32_t count, int32_t threads, const std::function<void(int32_t)>& f) {
+    std::lock_guard<std::mutex> job(job_mu_);
+    const int32_t helpers = std::max(0, std::min(threads, count) - 1);
+    while ((int32_t)workers_.size() < helpers) {
+      const int32_t id = (int32_t)workers_.size();
+      std::thread(&WorkerPool::loop, this, id).detach();
+      workers_.push_back(id);
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &f;
+      count_ = count;
+      next_.store(0);
+      helpers_ = helpers;
+      active_ = helpers;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return active_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const int32_t i = next_.fetch_add(1);
+      if (i >= count_) break;
+      (*fn_)(i);
+    }
+  }
+  void loop(int32_t id) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= helpers_) continue;  // not needed for this job
+      }
+      work();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--active_ == 0) done_cv_.notify_all();
+    }
+  }
+
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<int32_t> workers_;
+  const std::function<void(int32_t)>* fn_ = nullptr;
+  std::atomic<int32_t> next_{0};
+  int32_t count_ = 0, active_ = 0, helpers_ = 0;
+  uint64_t gen_ = 0;
+};
+
 template <typename F>
 void parallel_for(int32_t count, int32_t threads, F&& f) {
   if (threads <= 1 || count <= 1) {
     for (int32_t i = 0; i < count; ++i) f(i);
     return;
   }
-  threads = std::min(threads, count);
-  std::atomic<int32_t> next{0};
-  std::vector<std::thread> pool;
-  pool.reserve(threads);
-  for (int32_t t = 0; t < threads; ++t)
-    pool.emplace_back([&]() {
-      for (;;) {
-        int32_t i = next.fetch_add(1);
-        if (i >= count) break;
-        f(i);
-      }
-    });
-  for (auto& th : pool) th.join();
+  const std::function<void(int32_t)> fn = f;
+  WorkerPool::get().run(count, threads, fn);
 }
 
 // ---- torchac-compatible arithmetic coder ------------------------------------

@@ -880,6 +880,92 @@ int launch_ring_auto(const ConvArgs& a, hipStream_t s) {
   return -1;
 }
 
+// ============================================================================================
+// Tiny-cout direct 3x3 conv (cout <= 4; the VAE decoder's conv_out 128 -> 3 with GroupNorm +
+// SiLU on its input). An MFMA tile would compute 16 columns for 3 useful ones and re-apply GN on
+// every gathered element, so this is a VALU kernel instead: a 256-thread block owns a 16x16
+// output patch; per 32-channel chunk the 18x18 input halo is staged once into LDS (GN affine +
+// SiLU applied there, rounded to bf16 exactly like the materialised GN path), the chunk's
+// weights go to LDS as fp32, and each thread accumulates its pixel's COUT outputs in fp32.
+// HBM traffic ~= one read of the input (+ halo) and one write of the output.
+// ============================================================================================
+template <int COUT>
+__global__ __launch_bounds__(256) void conv3x3_smallc_kernel(ConvArgs a) {
+  constexpr int CC = 32, PS = 40;  // channels per chunk; LDS pixel stride in bf16 (80 B: bank spread)
+  __shared__ __attribute__((aligned(16))) bf16 xs[18 * 18 * PS];
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  const int img = blockIdx.z;
+  const int oy0 = blockIdx.y * 16, ox0 = blockIdx.x * 16;
+  const int cin = a.c0;
+  float acc[COUT];
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) acc[o] = 0.f;
+  const bf16* in = reinterpret_cast<const bf16*>(a.in0);
+  for (int c0 = 0; c0 < cin; c0 += CC) {
+    __syncthreads();
+    // stage 18x18 pixels x 32 channels = 1296 chunks of 8 channels
+    for (int q = tid; q < 18 * 18 * (CC / 8); q += 256) {
+      const int p = q >> 2, ch = (q & 3) * 8;
+      const int py = p / 18, px = p - py * 18;
+      const int iy = oy0 + py - 1, ix = ox0 + px - 1;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w && c0 + ch < cin) {
+        v = *reinterpret_cast<const uint4*>(in + (((long)img * a.h + iy) * a.w + ix) * a.ld0 + c0 + ch);
+        if (a.gn_ab) v = gn_apply_chunk<bf16>(v, a.gn_ab + ((long)img * cin + c0 + ch) * 2, a.gn_silu);
+      }
+      *reinterpret_cast<uint4*>(xs + p * PS + ch) = v;
+    }
+    __syncthreads();
+    // weights are wave-uniform: scalar loads of the packed bf16 rows (k = (ky*3+kx)*cin + ci)
+    const bf16* wp = reinterpret_cast<const bf16*>(a.weight);
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - ky * 3;
+      const bf16* xp = xs + ((ty + ky) * 18 + tx + kx) * PS;
+#pragma unroll
+      for (int c8 = 0; c8 < CC; c8 += 8) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xp + c8);
+        bf16x8 wv[COUT];
+#pragma unroll
+        for (int o = 0; o < COUT; ++o)
+          wv[o] = *reinterpret_cast<const bf16x8*>(wp + (long)o * a.wld + t * cin + c0 + c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = (float)xv[e];
+#pragma unroll
+          for (int o = 0; o < COUT; ++o) acc[o] = fmaf(x, (float)wv[o][e], acc[o]);
+        }
+      }
+    }
+  }
+  const int oy = oy0 + ty, ox = ox0 + tx;
+  if (oy >= a.ho || ox >= a.wo) return;
+  const long m = ((long)img * a.ho + oy) * a.wo + ox;
+#pragma unroll
+  for (int o = 0; o < COUT; ++o) {
+    if (o >= a.cout) break;
+    float v = acc[o];
+    if (a.bias) v += a.bias[o];
+    v = apply_act(v, a.act, a.act_param);
+    if (a.res) v += a.out_f32 ? reinterpret_cast<const float*>(a.res)[m * a.res_ld + o]
+                              : to_f32(reinterpret_cast<const bf16*>(a.res)[m * a.res_ld + o]);
+    if (a.out_f32) reinterpret_cast<float*>(a.out)[m * a.out_ld + o] = v;
+    else reinterpret_cast<bf16*>(a.out)[m * a.out_ld + o] = from_f32<bf16>(v);
+  }
+}
+
+int launch_smallc(const ConvArgs& a, hipStream_t s) {
+  dim3 grid(cdiv(a.wo, 16), cdiv(a.ho, 16), a.n);
+  switch (a.cout) {
+    case 1: hipLaunchKernelGGL(conv3x3_smallc_kernel<1>, grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(conv3x3_smallc_kernel<2>, grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(conv3x3_smallc_kernel<3>, grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(conv3x3_smallc_kernel<4>, grid, dim3(256), 0, s, a); break;
+  }
+  return launch_status();
+}
+
 }  // namespace
 
 extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
@@ -924,6 +1010,10 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
     if (a.M <= 8192) return launch_glds<64, 128, 2, 2, 3>(a, s);
     return launch_glds<128, 128, 2, 2, 3>(a, s);
   }
+  if (d->dtype == 1 && vec && d->cout <= 4 && d->c0 % 32 == 0 && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad_t == 1 &&
+      d->pad_l == 1 && !d->up2 && !d->c1 && d->out_mode == 0 && a.batch == 1 && d->ho == d->h && d->wo == d->w &&
+      g_conv_path != 0)
+    return launch_smallc(a, s);
   if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 3) {
     const int rc = launch_ring_auto(a, s);
     if (rc != -1) return rc;

@@ -91,8 +91,24 @@ __global__ __launch_bounds__(256) void gn_partial_vec_kernel(const bf16* __restr
     bf16x8 k = *reinterpret_cast<const bf16x8*>(xi + q * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) K[e] = (float)k[e];
-    for (int p = p0 + pl; p < p1; p += PL) {
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(xi + (long)p * ld + q * 8);
+    // four independent 16-byte loads in flight per thread; accumulation stays in pixel order
+    int p = p0 + pl;
+    const bf16* xq = xi + q * 8;
+    for (; p + 3 * PL < p1; p += 4 * PL) {
+      bf16x8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const bf16x8*>(xq + (long)(p + u * PL) * ld);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = (float)v[u][e] - K[e];
+          s1[e] += d;
+          s2[e] += d * d;
+        }
+    }
+    for (; p < p1; p += PL) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(xq + (long)p * ld);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float d = (float)v[e] - K[e];
@@ -117,49 +133,63 @@ __global__ __launch_bounds__(256) void gn_partial_vec_kernel(const bf16* __restr
   }
 }
 
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// pass 2, one 256-thread block per (group, image): the (chunk, channel) partials of the group are
+// spread over all threads (fixed assignment, fixed tree order -> deterministic). With K_ch the
+// per-channel shift, S1_ch = sum_q s1[q][ch], S2_ch likewise:
+//   mean = (sum_ch S1_ch + cnt * sum_ch K_ch) / N
+//   M2   = sum_ch S2_ch + 2 sum_ch d_ch S1_ch + cnt sum_ch d_ch^2,   d_ch = K_ch - mean
 template <typename T>
-__global__ __launch_bounds__(64) void gn_finalize_kernel(const T* __restrict__ x0, int c0, int ld0,
-                                                         const T* __restrict__ x1, int ld1, int hw, int c, int groups,
-                                                         int nchunk, const float* __restrict__ part, float eps,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float* __restrict__ ab) {
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const T* __restrict__ x0, int c0, int ld0,
+                                                          const T* __restrict__ x1, int ld1, int hw, int c, int groups,
+                                                          int nchunk, const float* __restrict__ part, float eps,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ ab) {
   const int img = blockIdx.y, g = blockIdx.x;
   const int cpg = c / groups;
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x;
   const float cnt = (float)hw;
-  float s1c[8], s2c[8], Kc[8];  // cpg <= 512 -> up to 8 channels per lane
-  int nmine = 0;
-  for (int j = lane; j < cpg; j += 64, ++nmine) {
-    int ch = g * cpg + j;
-    float s1 = 0.f, s2 = 0.f;
-    for (int q = 0; q < nchunk; ++q) {
-      const float* pp = part + (((long)img * nchunk + q) * c + ch) * 2;
-      s1 += pp[0];
-      s2 += pp[1];
-    }
-    s1c[nmine] = s1;
-    s2c[nmine] = s2;
-    Kc[nmine] = load_seg(x0, c0, ld0, x1, ld1, (long)img * hw, ch);
+  __shared__ float Ks[512];
+  __shared__ float red[4];
+  for (int j = t; j < cpg; j += 256) Ks[j] = load_seg(x0, c0, ld0, x1, ld1, (long)img * hw, g * cpg + j);
+  __syncthreads();
+  const int pairs = nchunk * cpg;
+  const float* pb = part + ((long)img * nchunk * c + g * cpg) * 2;
+  float a1 = 0.f, ks = 0.f;
+  for (int i = t; i < pairs; i += 256) {
+    const int q = i / cpg, j = i - q * cpg;
+    a1 += pb[((long)q * c + j) * 2];
   }
-  float tot = 0.f;
-  for (int q = 0; q < nmine; ++q) tot += s1c[q] + cnt * Kc[q];
-  tot = warp_sum(tot);
+  for (int j = t; j < cpg; j += 256) ks += Ks[j];
   const float n_el = cnt * (float)cpg;
-  const float mean = tot / n_el;
-  float m2 = 0.f;
-  for (int q = 0; q < nmine; ++q) {
-    float d = Kc[q] - mean;
-    m2 += s2c[q] + 2.f * d * s1c[q] + cnt * d * d;
+  const float mean = (block_sum256(a1, red) + cnt * block_sum256(ks, red)) / n_el;
+  float a2 = 0.f, dd = 0.f;
+  for (int i = t; i < pairs; i += 256) {
+    const int q = i / cpg, j = i - q * cpg;
+    const float* pp = pb + ((long)q * c + j) * 2;
+    a2 += pp[1] + 2.f * (Ks[j] - mean) * pp[0];
   }
-  m2 = warp_sum(m2);
+  for (int j = t; j < cpg; j += 256) {
+    const float d = Ks[j] - mean;
+    dd += d * d;
+  }
+  const float m2 = block_sum256(a2, red) + cnt * block_sum256(dd, red);
   const float var = fmaxf(m2 / n_el, 0.f);
   const float rstd = rsqrtf(var + eps);
-  for (int j = lane; j < cpg; j += 64) {
-    int ch = g * cpg + j;
-    float ga = gamma ? gamma[ch] : 1.f, be = beta ? beta[ch] : 0.f;
-    float a = ga * rstd;
-    ab[((long)img * c + ch) * 2 + 0] = a;
-    ab[((long)img * c + ch) * 2 + 1] = be - mean * a;
+  for (int j = t; j < cpg; j += 256) {
+    const int ch = g * cpg + j;
+    const float ga = gamma ? gamma[ch] : 1.f, be = beta ? beta[ch] : 0.f;
+    const float av = ga * rstd;
+    ab[((long)img * c + ch) * 2 + 0] = av;
+    ab[((long)img * c + ch) * 2 + 1] = be - mean * av;
   }
 }
 
@@ -180,29 +210,97 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
   }
 }
 
-// 16-byte vectorised variant: one thread = 8 bf16 channels of one pixel (c, ld, yld multiples of 8)
+// 16-byte vectorised variant: one thread = 8 bf16 channels of one pixel (c, ld, yld multiples of 8);
+// grid (x, image), 32-bit indexing inside an image, 4 chunks per thread for loads in flight.
 __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const bf16* __restrict__ x, int n, int hw, int c, int ld,
                                                            const float* __restrict__ ab, int ab_c, int silu,
                                                            float out_mul, bf16* __restrict__ y, int yld) {
   const int cp = c >> 3;
-  long total = (long)n * hw * cp;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    long pix = i / cp;
-    int ch = (int)(i - pix * cp) * 8;
-    int img = (int)(pix / hw);
-    const float4* p = reinterpret_cast<const float4*>(ab + ((long)img * ab_c + ch) * 2);
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(x + pix * ld + ch);
+  const int img = blockIdx.y;
+  const int total = hw * cp;
+  const bf16* xi = x + (long)img * hw * ld;
+  bf16* yi = y + (long)img * hw * yld;
+  const float* abi = ab + (long)img * ab_c * 2;
+  const int base = blockIdx.x * 1024 + threadIdx.x;
+  bf16x8 v[4];
+  int pix[4], ch[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = base + u * 256;
+    pix[u] = i / cp;
+    ch[u] = (i - pix[u] * cp) * 8;
+    if (i < total) v[u] = *reinterpret_cast<const bf16x8*>(xi + (long)pix[u] * ld + ch[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (base + u * 256 >= total) break;
+    const float4* p = reinterpret_cast<const float4*>(abi + ch[u] * 2);
     bf16x8 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float4 s = p[q];  // (a, b) of channels ch+2q, ch+2q+1
-      float v0 = (float)v[2 * q] * s.x + s.y;
-      float v1 = (float)v[2 * q + 1] * s.z + s.w;
+      float v0 = (float)v[u][2 * q] * s.x + s.y;
+      float v1 = (float)v[u][2 * q + 1] * s.z + s.w;
       if (silu) { v0 = silu_f(v0); v1 = silu_f(v1); }
       o[2 * q] = (bf16)(v0 * out_mul);
       o[2 * q + 1] = (bf16)(v1 * out_mul);
     }
-    *reinterpret_cast<bf16x8*>(y + pix * yld + ch) = o;
+    *reinterpret_cast<bf16x8*>(yi + (long)pix[u] * yld + ch[u]) = o;
+  }
+}
+
+// LayerNorm, bf16, c % 8 == 0, c <= 2048: one wave per row, the row held in registers (one HBM
+// read), 4 rows per 256-thread block.
+__global__ __launch_bounds__(256) void layernorm_vec_kernel(const bf16* __restrict__ x, int rows, int c, int ld,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps,
+                                                            bf16* __restrict__ y, int yld) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int cp = c >> 3;
+  const bf16* xr = x + (long)row * ld;
+  bf16x8 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = lane + u * 64;
+    if (k < cp) {
+      v[u] = *reinterpret_cast<const bf16x8*>(xr + k * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)v[u][e];
+    }
+  }
+  s = warp_sum(s);
+  const float mean = s / c;
+  float v2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = lane + u * 64;
+    if (k < cp) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (float)v[u][e] - mean;
+        v2 += d * d;
+      }
+    }
+  }
+  v2 = warp_sum(v2);
+  const float rstd = rsqrtf(v2 / c + eps);
+  bf16* yr = y + (long)row * yld;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = lane + u * 64;
+    if (k < cp) {
+      const float4 g0 = *reinterpret_cast<const float4*>(gamma + k * 8), g1 = *reinterpret_cast<const float4*>(gamma + k * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(beta + k * 8), b1 = *reinterpret_cast<const float4*>(beta + k * 8 + 4);
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)(((float)v[u][e] - mean) * rstd * gg[e] + bb[e]);
+      *reinterpret_cast<bf16x8*>(yr + k * 8) = o;
+    }
   }
 }
 
@@ -248,7 +346,7 @@ int gn_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1
   };
   seg(x0, c0, ld0, 0);
   if (c1 > 0) seg(x1, c1, ld1, c0);
-  hipLaunchKernelGGL(gn_finalize_kernel<T>, dim3(groups, n), dim3(64), 0, s, (const T*)x0, c0, ld0,
+  hipLaunchKernelGGL(gn_finalize_kernel<T>, dim3(groups, n), dim3(256), 0, s, (const T*)x0, c0, ld0,
                      (const T*)(x1 ? x1 : x0), c1 > 0 ? ld1 : ld0, hw, c, groups, nchunk, ws, eps, gamma, beta, ab);
   return launch_status();
 }
@@ -280,8 +378,9 @@ extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32
   long total = (long)n * hw * c;
   if (dtype == 1 && c % 8 == 0 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
       ((uintptr_t)y) % 16 == 0 && ((uintptr_t)ab) % 16 == 0) {
-    int blocks = (int)std::min<long>((total / 8 + 255) / 256, 16384);
-    hipLaunchKernelGGL(gn_apply_vec_kernel, dim3(blocks), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld, ab, ab_c,
+    if ((long)hw * (c / 8) >= (1L << 31) - 2048) return RDEIC_EINVAL;
+    const int blocks = (int)(((long)hw * (c / 8) + 1023) / 1024);
+    hipLaunchKernelGGL(gn_apply_vec_kernel, dim3(blocks, n), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld, ab, ab_c,
                        silu, out_mul, (bf16*)y, yld);
     return launch_status();
   }
@@ -299,7 +398,11 @@ extern "C" int rdeic_layernorm(const void* x, int32_t rows, int32_t c, int32_t l
                                const float* beta, float eps, void* y, int32_t yld, int32_t dtype, void* stream) {
   if (!x || !y || !gamma || !beta || rows <= 0 || c <= 0) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == 1)
+  if (dtype == 1 && c % 8 == 0 && c <= 2048 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
+      ((uintptr_t)y) % 16 == 0 && ((uintptr_t)gamma) % 16 == 0 && ((uintptr_t)beta) % 16 == 0)
+    hipLaunchKernelGGL(layernorm_vec_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, (const bf16*)x, rows, c, ld, gamma,
+                       beta, eps, (bf16*)y, yld);
+  else if (dtype == 1)
     hipLaunchKernelGGL(layernorm_kernel<bf16>, dim3(rows), dim3(64), 0, s, (const bf16*)x, rows, c, ld, gamma, beta,
                        eps, (bf16*)y, yld);
   else

@@ -14,7 +14,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "e2e
 def run_smoke():
     assert torch.cuda.is_available(), "smoke() needs a GPU"
     from rdeic_amd import _lib
-    _lib.lib()  # loud failure if the HIP library is missing
+    _lib.load()  # loud failure if the HIP library is missing
     from rdeic_amd.rdeic import RDEIC
     from oracle import model_ref as M
 

@@ -190,3 +190,50 @@ def test_fill_uniform_matches_oracle(gpu):
     ops.fill_uniform(out, 123456789, 0.05, 1.0)
     ref = weights_cpu.fill_uniform(n, 123456789, 0.05, 1.0)
     assert torch.equal(out.cpu(), torch.from_numpy(ref))
+
+
+@pytest.mark.parametrize("c,hw", [(128, 45), (256, 33), (96, 70)])
+def test_groupnorm_large_bf16(gpu, c, hw):
+    """Several pass-1 chunks per image (unrolled pixel loop + tail), parallel finalize."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(c * hw)
+    x = torch.randn(3, c, hw, hw + 3, generator=g) * 2 - 7
+    gamma = torch.rand(c, generator=g) + 0.5
+    beta = torch.randn(c, generator=g)
+    xq = x.to(torch.bfloat16).float()
+    ref = F.silu(F.group_norm(xq, 32, gamma, beta, eps=1e-6))
+    xd = _nhwc(x.to(torch.bfloat16))
+    ab = ops.group_norm_ab(xd, gamma.cuda(), beta.cuda(), 32, 1e-6)
+    out = ops.group_norm_apply(xd, ab, silu=True)
+    torch.testing.assert_close(_nchw(out), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("c", [320, 640, 1280, 1024])
+def test_layernorm_vec(gpu, c):
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(c)
+    x = torch.randn(301, c, generator=g) * 3 + 2
+    gamma, beta = torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g)
+    ref = F.layer_norm(x.to(torch.bfloat16).float(), (c,), gamma, beta, 1e-5)
+    out = ops.layer_norm(x.to(torch.bfloat16).cuda(), gamma.cuda(), beta.cuda(), 1e-5)
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("cout,h,w", [(3, 40, 37), (4, 16, 16), (1, 33, 20)])
+def test_conv_small_cout_gn(gpu, cout, h, w):
+    """Tiny-cout direct conv (VAE conv_out) with the GroupNorm + SiLU prologue."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(cout * h)
+    cin = 128
+    x = torch.randn(2, cin, h, w, generator=g) * 2 + 1
+    gamma, beta = torch.rand(cin, generator=g) + 0.5, torch.randn(cin, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    b = torch.randn(cout, generator=g)
+    xq = x.to(torch.bfloat16).float()
+    hn = F.silu(F.group_norm(xq, 32, gamma, beta, eps=1e-6)).to(torch.bfloat16).float()
+    ref = F.conv2d(hn, wt.to(torch.bfloat16).float(), b, padding=1)
+    xd = _nhwc(x.to(torch.bfloat16))
+    ab = ops.group_norm_ab(xd, gamma.cuda(), beta.cuda(), 32, 1e-6)
+    p = ops.ConvParams.pack(wt, b, pad=1, dtype=torch.bfloat16)
+    out = ops.conv2d(xd, p, gn=ab, gn_silu=True, out_f32=True)
+    torch.testing.assert_close(_nchw(out), ref, rtol=1e-2, atol=2e-2)
