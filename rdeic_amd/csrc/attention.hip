@@ -16,6 +16,8 @@
 #include "common.h"
 #include "../../include/rdeic_hip.h"
 
+int rdeic_g_attn64 = 1;  // rdeic_set_conv_option(1, v): transposed dh=64 kernel on/off
+
 namespace {
 
 constexpr int QT = 64;   // query rows per block
@@ -227,9 +229,209 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in
   }
 }
 
+// ============================================================================================
+// bf16, head dim 64: transposed formulation. Per 64-key tile a wave computes S^T = K Q^T for its
+// 32 queries (A = K fragment from LDS, B = Q fragment in registers), so an MFMA output lane holds
+// ONE query (lane & 15) and 4 keys. That is exactly the B-operand layout of O^T += V^T P^T once
+// the 32 keys of a k-step are taken in the order pi(8g + j) = 4g + j (j < 4), 16 + 4g + j - 4
+// (j >= 4): P never leaves registers, and the row max / sum need only the 4 lanes of a query
+// (2 shuffles). V^T is staged transposed in LDS (key pairs packed into 32-bit stores,
+// conflict-free), read as two 8-byte pieces per fragment. K / V^T tiles are double-buffered:
+// the next tile's global loads are in flight during the current tile's math, one barrier per
+// tile. 4 waves x 32 queries = 128 queries per block.
+// ============================================================================================
+constexpr int A64_Q = 128;  // queries per block
+constexpr int A64_ROW = 72;  // LDS row stride (elements) of the K and V^T tiles: 144 B
+
+__global__ __launch_bounds__(256) void attn64_kernel(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
+                                                     int ldk, const bf16* __restrict__ v, int ldv, bf16* __restrict__ o,
+                                                     int ldo, int heads, int lq, int lk, float scale_log2,
+                                                     int kv_bcast) {
+  __shared__ __attribute__((aligned(16))) bf16 Ks[2][64 * A64_ROW];
+  __shared__ __attribute__((aligned(16))) bf16 Vt[2][64 * A64_ROW];
+  const int bh = blockIdx.y;
+  const int b = bh / heads, h = bh - b * heads;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const bf16* qb = q + (long)b * lq * ldq + h * 64;
+  const long kvb = kv_bcast ? 0 : b;
+  const bf16* kb = k + kvb * lk * ldk + h * 64;
+  const bf16* vb = v + kvb * lk * ldv + h * 64;
+  const int qw = blockIdx.x * A64_Q + wave * 32;  // this wave's first query
+
+  // Q as the B operand: lane (query qw + 16u + lr, g) holds d = 32hd + 8g .. +8
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int hd = 0; hd < 2; ++hd) {
+      const int qq = qw + 16 * u + lr;
+      bf16x8 z = *reinterpret_cast<const bf16x8*>(qb + (long)min(qq, lq - 1) * ldq + 32 * hd + 8 * g);
+      if (qq >= lq) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
+      }
+      qf[u][hd] = z;
+    }
+
+  // staging assignment: K: 2 chunks (key = c >> 3, d-chunk = c & 7); V: key pair kp, d-chunk vc
+  const int kc0 = tid, kc1 = tid + 256;
+  const int kp = tid & 31, vc = tid >> 5;
+  uint4 kr0, kr1, va, vbv;
+  auto load_tile = [&](int key0) {
+    // loads always hit a valid row (clamped); out-of-range keys are zeroed by value select
+    const int k0 = key0 + (kc0 >> 3), k1 = key0 + (kc1 >> 3);
+    const int v0 = key0 + 2 * kp, v1 = v0 + 1;
+    kr0 = *reinterpret_cast<const uint4*>(kb + (long)min(k0, lk - 1) * ldk + (kc0 & 7) * 8);
+    kr1 = *reinterpret_cast<const uint4*>(kb + (long)min(k1, lk - 1) * ldk + (kc1 & 7) * 8);
+    va = *reinterpret_cast<const uint4*>(vb + (long)min(v0, lk - 1) * ldv + vc * 8);
+    vbv = *reinterpret_cast<const uint4*>(vb + (long)min(v1, lk - 1) * ldv + vc * 8);
+    const uint4 zz = make_uint4(0, 0, 0, 0);
+    if (k0 >= lk) kr0 = zz;
+    if (k1 >= lk) kr1 = zz;
+    if (v0 >= lk) va = zz;
+    if (v1 >= lk) vbv = zz;
+  };
+  auto store_tile = [&](int buf) {
+    *reinterpret_cast<uint4*>(&Ks[buf][(kc0 >> 3) * A64_ROW + (kc0 & 7) * 8]) = kr0;
+    *reinterpret_cast<uint4*>(&Ks[buf][(kc1 >> 3) * A64_ROW + (kc1 & 7) * 8]) = kr1;
+    const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vbv.x, vbv.y, vbv.z, vbv.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&Vt[buf][(vc * 8 + 2 * w) * A64_ROW + 2 * kp]);
+      dst[0] = (wa[w] & 0xffffu) | (wb[w] << 16);                      // d = 8vc + 2w: (key 2kp, 2kp+1)
+      dst[A64_ROW / 2] = (wa[w] >> 16) | (wb[w] & 0xffff0000u);        // d = 8vc + 2w + 1
+    }
+  };
+
+  f32x4 oacc[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+
+  const int ntiles = (lk + 63) / 64;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int buf = kt & 1;
+    const int key0 = kt * 64;
+    if (kt + 1 < ntiles) load_tile(key0 + 64);
+    // ---- S^T[key][query] for 4 key sub-tiles x 2 query tiles
+    f32x4 st[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf16* kr = &Ks[buf][(16 * t + lr) * A64_ROW + 8 * g];
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kr);
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kr + 32);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[u][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[u][1], acc, 0, 0, 0);
+        st[u][t] = acc;
+      }
+    }
+    // ---- online softmax per query (lane's query; keys 16t + 4g + i). Scores are used in the
+    // log2 domain (scale folded into one FMA). The running max m only moves when the tile max
+    // exceeds it by more than 8 (P <= 2^8 otherwise, exact in fp32 / bf16 range): most tiles
+    // then skip the O rescale entirely (wave-uniform test).
+    if (key0 + 64 > lk) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (key0 + 16 * t + 4 * g + i >= lk) st[u][t][i] = -INFINITY;
+    }
+    bf16x8 pf[2][2];
+    bool rescale = false;
+    float alpha[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mx = st[u][0][0];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[u][t][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float ms = mx * scale_log2;
+      alpha[u] = 1.f;
+      if (ms > m_run[u] + 8.f) {
+        alpha[u] = __builtin_amdgcn_exp2f(m_run[u] - ms);
+        m_run[u] = ms;
+        rescale = true;
+      }
+      const float nm = -m_run[u];
+      float ps = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[u][2 * c + (j >> 2)][j & 3], scale_log2, nm));
+          ps += p;
+          pf[u][c][j] = (bf16)p;
+        }
+      l_run[u] = l_run[u] * alpha[u] + ps;
+    }
+    if (__any(rescale)) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) oacc[u][dt] *= alpha[u];
+    }
+    // ---- O^T[d][query] += V^T P^T, keys of k-step c in the order pi
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16* vr = &Vt[buf][(16 * dt + lr) * A64_ROW + 4 * g];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr + 32 * c);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 32 * c + 16);
+        const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) oacc[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[u][c], oacc[u][dt], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < ntiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+  // ---- finalize: lane (query, g) holds d = 16dt + 4g + i
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float l = l_run[u];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+    const int qq = qw + 16 * u + lr;
+    if (qq < lq) {
+      bf16* orow = o + ((long)b * lq + qq) * ldo + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 ov;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ov[i] = (bf16)(oacc[u][dt][i] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = ov;
+      }
+    }
+  }
+}
+
 template <typename T>
 int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo, int batch,
                 int heads, int lq, int lk, int dh, float scale, int kv_bcast, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (dh == 64 && rdeic_g_attn64 && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0) {
+      dim3 grid((lq + A64_Q - 1) / A64_Q, batch * heads);
+      hipLaunchKernelGGL(attn64_kernel, grid, dim3(256), 0, s, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v,
+                         ldv, (bf16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_bcast);
+      return launch_status();
+    }
+  }
   dim3 grid((lq + QT - 1) / QT, batch * heads);
   float sl2 = scale * 1.4426950408889634f;
 #define ATTN_CASE(D)                                                                                              \

@@ -42,6 +42,10 @@ struct ConvArgs {
   int epi_vec;               // 1: LDS-staged vector epilogue where eligible
 };
 
+int g_conv_path = 2;  // 0: register-staged + fused GN, 1: LDS-DMA ring, 2: register-staged big tiles
+int g_epi_vec = 1;    // LDS-staged vector epilogue (rdeic_set_conv_option(0, v))
+int g_pf2 = 0;        // 2-deep register prefetch in the plain path (rdeic_set_conv_option(2, v)); measured neutral, off
+
 constexpr int ROWB = 144;  // LDS bytes per tile row: 128 B of k-data + 16 B pad (bank spread)
 
 template <typename T> struct MmaTraits;
@@ -166,7 +170,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
 }
 
 // GNP: compile the GroupNorm+SiLU gather prologue in (false = plain gather, fewer VGPRs / VALU).
-template <typename T, int BM, int BN, int WGM, int WGN, bool VEC, bool GNP = true>
+template <typename T, int BM, int BN, int WGM, int WGN, bool VEC, bool GNP = true, bool PF2 = false>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int BK = MmaTraits<T>::BK;
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
   uint4 breg[BR];
   int a_c[AR];  // channel of chunk start per row (for the GN prologue), -1 = zero chunk
 
-  auto gather_a = [&](int kt) {
+  auto gather_a = [&](int kt, uint4 (&areg)[AR]) {
     const int k0 = kt * BK + kc * EPC;
     if constexpr (VEC) {
       bool kval = k0 < a.ktot;
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
     }
   };
 
-  auto gather_b = [&](int kt) {
+  auto gather_b = [&](int kt, uint4 (&breg)[BR]) {
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       int cid = tid + NT * i;
@@ -289,7 +293,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
     }
   };
 
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, const uint4 (&areg)[AR], const uint4 (&breg)[BR]) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       uint4 v = areg[i];
@@ -316,14 +320,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 
   const int lrow = lane & 15, lq = lane >> 4;
 
-  gather_a(0);
-  gather_b(0);
-  store_tiles(0);
-  __syncthreads();
-
-  for (int kt = 0; kt < a.nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < a.nk) { gather_a(kt + 1); gather_b(kt + 1); }
+  auto compute = [&](int cur) {
     const char* Ab = AS(cur) + (wm * WTM + lrow) * ROWB;
     const char* Bb = BS(cur) + (wn * WTN + lrow) * ROWB;
     if constexpr (sizeof(T) == 2) {
@@ -369,8 +366,40 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (kt + 1 < a.nk) store_tiles(cur ^ 1);
+  };
+
+  if constexpr (PF2) {
+    // two register sets: tile j lives in set j & 1; the load of tile k+2 is in flight while
+    // tile k is computed and tile k+1 (loaded one step earlier) is written to LDS.
+    uint4 ary[AR], bry[BR];
+    gather_a(0, areg); gather_b(0, breg);
+    store_tiles(0, areg, breg);
+    if (a.nk > 1) { gather_a(1, ary); gather_b(1, bry); }
     __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < a.nk; kt += 2) {
+      if (kt + 2 < a.nk) { gather_a(kt + 2, areg); gather_b(kt + 2, breg); }
+      compute(0);
+      store_tiles(1, ary, bry);
+      __syncthreads();
+      if (kt + 3 < a.nk) { gather_a(kt + 3, ary); gather_b(kt + 3, bry); }
+      compute(1);
+      if (kt + 2 < a.nk) store_tiles(0, areg, breg);
+      __syncthreads();
+    }
+    if (kt < a.nk) compute(0);
+  } else {
+    gather_a(0, areg);
+    gather_b(0, breg);
+    store_tiles(0, areg, breg);
+    __syncthreads();
+    for (int kt = 0; kt < a.nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < a.nk) { gather_a(kt + 1, areg); gather_b(kt + 1, breg); }
+      compute(cur);
+      if (kt + 1 < a.nk) store_tiles(cur ^ 1, areg, breg);
+      __syncthreads();
+    }
   }
 
 #undef AS
@@ -440,7 +469,13 @@ template <int BM, int BN, int WGM, int WGN>
 int launch_plain(const ConvArgs& a, hipStream_t s) {
   dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
   size_t lds = 2 * (BM + BN) * ROWB;
-  hipLaunchKernelGGL((conv_kernel<bf16, BM, BN, WGM, WGN, true, false>), grid, dim3(WGM * WGN * 64), lds, s, a);
+  // 2-deep register prefetch where the register budget allows it (<= 8 waves per block)
+  constexpr bool PF = (WGM * WGN <= 8);
+  if (PF && g_pf2)
+    hipLaunchKernelGGL((conv_kernel<bf16, BM, BN, WGM, WGN, true, false, PF>), grid, dim3(WGM * WGN * 64), lds, s, a);
+  else
+    hipLaunchKernelGGL((conv_kernel<bf16, BM, BN, WGM, WGN, true, false, false>), grid, dim3(WGM * WGN * 64), lds, s,
+                       a);
   return launch_status();
 }
 
@@ -481,8 +516,6 @@ int launch_plain_auto(const ConvArgs& a, hipStream_t s) {
 // No GroupNorm prologue here: GN+SiLU inputs are materialised by rdeic_groupnorm_apply first.
 // ============================================================================================
 __device__ uint4 g_zero_page[64];  // 1 KiB of zeros: source of every padded / out-of-range chunk
-int g_conv_path = 2;  // 0: register-staged + fused GN, 1: LDS-DMA ring, 2: register-staged big tiles
-int g_epi_vec = 1;    // LDS-staged vector epilogue (rdeic_set_conv_option(0, v))
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -1038,7 +1071,11 @@ extern "C" int rdeic_set_conv_path(int32_t path) {
   return prev;
 }
 
+extern int rdeic_g_attn64;
+
 extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 0) { int prev = g_epi_vec; g_epi_vec = value; return prev; }
+  if (key == 1) { int prev = rdeic_g_attn64; rdeic_g_attn64 = value; return prev; }
+  if (key == 2) { int prev = g_pf2; g_pf2 = value; return prev; }
   return RDEIC_EINVAL;
 }

@@ -24,6 +24,8 @@ SHAPES = [  # (name, B, H, W, cin, cout, k, stride)
     ("vae512@128", 16, 128, 128, 512, 512, 3, 1),
     ("vae512@64", 16, 64, 64, 512, 512, 3, 1),
     ("linear320x1280 (ff)", 16, 64, 64, 320, 2560, 1, 1),
+    ("linear320x320", 16, 64, 64, 320, 320, 1, 1),
+    ("vae256to128@512", 16, 512, 512, 256, 128, 3, 1),
 ]
 
 
@@ -42,6 +44,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--paths", default="0,1,2")
     ap.add_argument("--epi", default="1", help="comma list of epilogue modes to A/B (1 vector, 0 scalar)")
+    ap.add_argument("--pf2", default="1", help="comma list of register-prefetch modes to A/B (1 two-deep, 0 one)")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []
@@ -52,28 +55,32 @@ def main():
         w = torch.randn(cout, cin, k, k, device="cuda") / math.sqrt(cin * k * k)
         p = ops.ConvParams.pack(w, torch.randn(cout, device="cuda"), stride=stride, pad=k // 2)
         res_t = torch.randn(B, H // stride, W // stride, cout, device="cuda").to(torch.bfloat16)
-        paths = [(int(v), int(e)) for v in args.paths.split(",") for e in args.epi.split(",")]
+        paths = [(int(v), int(e), int(f)) for v in args.paths.split(",") for e in args.epi.split(",")
+                 for f in args.pf2.split(",")]
         outs = {}
         times = {q: [] for q in paths}
         fn = lambda: ops.conv2d(x, p, res=res_t, act=ops.SILU)  # noqa: E731
-        for path, epi in paths:
+        for path, epi, pf in paths:
             ops.set_conv_path(path)
             ops.set_conv_option(0, epi)
-            outs[(path, epi)] = fn()
+            ops.set_conv_option(2, pf)
+            outs[(path, epi, pf)] = fn()
         for _ in range(3):
-            for path, epi in paths:
+            for path, epi, pf in paths:
                 ops.set_conv_path(path)
                 ops.set_conv_option(0, epi)
-                times[(path, epi)].append(bench(fn, args.reps))
+                ops.set_conv_option(2, pf)
+                times[(path, epi, pf)].append(bench(fn, args.reps))
         flops = 2.0 * B * (H // stride) * (W // stride) * cout * cin * k * k
         r = dict(name=name)
         for q in paths:
-            r[f"tflops_p{q[0]}e{q[1]}"] = round(flops / min(times[q]) / 1e12, 1)
+            r[f"tflops_p{q[0]}e{q[1]}f{q[2]}"] = round(flops / min(times[q]) / 1e12, 1)
         r["identical"] = all(torch.equal(outs[paths[0]], outs[q]) for q in paths)
         print(json.dumps(r), flush=True)
         res.append(r)
     ops.set_conv_path(2)
     ops.set_conv_option(0, 1)
+    ops.set_conv_option(2, 1)
 
 
 if __name__ == "__main__":

@@ -39,20 +39,33 @@ def main():
         ops.set_conv_path(path)
         model.codec_images(imgs, ctx, noise, steps=2)  # warmup
         stages = {}
+        marks = {}
         ops.PROFILE = []
-        h, stages["encode_vae"] = timed(lambda: model.encode_images_nhwc(imgs))
-        outs, stages["compress_nets+coder"] = timed(lambda: model.preprocess_model.compress(h))
+
+        def timed_stage(name, fn):
+            n0 = len(ops.PROFILE)
+            r, stages[name] = timed(fn)
+            marks[name] = (n0, len(ops.PROFILE))
+            return r
+
+        h = timed_stage("encode_vae", lambda: model.encode_images_nhwc(imgs))
+        outs = timed_stage("compress_nets+coder", lambda: model.preprocess_model.compress(h))
         from rdeic_amd import bitstream
         bodies = [bitstream.pack_body(o["shape"], o["strings"]) for o in outs]
-        (c_lat, hint), stages["decompress"] = timed(lambda: model.decompress_bodies(bodies))
+        c_lat, hint = timed_stage("decompress", lambda: model.decompress_bodies(bodies))
         nz = ops.nchw_to_nhwc(noise.cuda(), torch.float32)
-        z, stages["relay_sample_2steps"] = timed(lambda: model.relay_sample_nhwc(c_lat, hint, ctx, nz, 2))
-        x, stages["vae_decode"] = timed(lambda: model.decode_nhwc(z))
-        _, stages["to_u8"] = timed(lambda: model.to_image_u8(x))
+        z = timed_stage("relay_sample_2steps", lambda: model.relay_sample_nhwc(c_lat, hint, ctx, nz, 2))
+        x = timed_stage("vae_decode", lambda: model.decode_nhwc(z))
+        timed_stage("to_u8", lambda: model.to_image_u8(x))
         torch.cuda.synchronize()
         prof, ops.PROFILE = ops.PROFILE, None
         n, flops, ms = ops.conv_profile_summary(prof)
+        conv_stage = {}
+        for k, (a0, a1) in marks.items():
+            _, f, m = ops.conv_profile_summary(prof[a0:a1]) if a1 > a0 else (0, 0.0, 0.0)
+            conv_stage[k] = round(m, 2)
         print(json.dumps({"conv_path": path, "stages_ms": {k: round(v, 2) for k, v in stages.items()},
+                          "conv_ms_by_stage": conv_stage,
                           "total_ms": round(sum(stages.values()), 2), "conv_launches": n,
                           "conv_ms": round(ms, 2), "conv_tflops": round(flops / ms / 1e9, 1)}), flush=True)
         bd = ops.conv_profile_breakdown(prof)
