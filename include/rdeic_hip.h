@@ -72,8 +72,10 @@ typedef struct rdeic_conv_desc {
 } rdeic_conv_desc;
 
 int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
-/* 1 (default): bf16 convs without a GN prologue use the LDS-DMA pipelined kernel; 0: the
- * register-staged kernel everywhere (A/B timing, debugging). Returns the previous value. */
+/* 2 (default): bf16 convs without a GN prologue pick among the big register-staged tiles
+ * (256x256 / 256x128 / 128x256 / 128x128 / 64x128 / 128x64); 0: the 128-tile kernel with the
+ * fused GroupNorm prologue everywhere (A/B timing, debugging). Results are bit-identical.
+ * Returns the previous value. */
 int rdeic_set_conv_path(int32_t path);
 /* Tuning switches (process-wide). key 0: LDS-staged vector epilogue on (1, default) / off (0);
  * key 1: transposed head-dim-64 attention kernel on (1, default) / off (0);

@@ -42,11 +42,28 @@ struct ConvArgs {
   int epi_vec;               // 1: LDS-staged vector epilogue where eligible
 };
 
-int g_conv_path = 2;  // 0: register-staged + fused GN, 1: LDS-DMA ring, 2: register-staged big tiles
+int g_conv_path = 2;  // 0: 128-tiles with the fused GroupNorm prologue only, 2 (default): big-tile auto choice
 int g_epi_vec = 1;    // LDS-staged vector epilogue (rdeic_set_conv_option(0, v))
 int g_pf2 = 0;        // 2-deep register prefetch in the plain path (rdeic_set_conv_option(2, v)); measured neutral, off
 
-constexpr int ROWB = 144;  // LDS bytes per tile row: 128 B of k-data + 16 B pad (bank spread)
+constexpr int ROWB = 144;  // fp32 tiles: LDS bytes per row, 128 B of k-data + 16 B pad (bank spread)
+
+// bf16 tiles use unpadded 128-byte rows with the 16-byte chunks XOR-swizzled by row bits 1 and 3:
+// chunk c of row r lives in slot c ^ key(r); every ds_read_b128 lane group of the 16x16x32
+// fragment reads (rows r..r+15, one chunk column) then covers all 64 banks once, and a row's
+// 8 chunks written by 8 lanes still cover 32 banks. Rows a lane touches differ by multiples of
+// 16, so key(r) is a per-lane constant on both sides.
+template <typename T> __host__ __device__ constexpr int tile_rowb() { return sizeof(T) == 2 ? 128 : ROWB; }
+template <typename T> __device__ __forceinline__ int chunk_key(int r) {
+  if constexpr (sizeof(T) == 2) return (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2);
+  return 0;
+}
+// dynamic LDS of conv_kernel: the double-buffered tiles, or the vector epilogue's half tile
+template <typename T, int BM, int BN> __host__ __device__ constexpr int conv_lds_bytes() {
+  return (2 * (BM + BN) * tile_rowb<T>() > (BM / 2) * (BN + 4) * 4 || sizeof(T) != 2)
+             ? 2 * (BM + BN) * tile_rowb<T>()
+             : (BM / 2) * (BN + 4) * 4;
+}
 
 template <typename T> struct MmaTraits;
 template <> struct MmaTraits<bf16> {
@@ -184,9 +201,10 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
   static_assert(TM >= 1 && TN >= 1 && AR >= 1 && BM % RPI == 0, "tile");
 
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  // buffer b: A tile at lds + b*(BM+BN)*ROWB, B tile right after it
-#define AS(b) (lds + (b) * (BM + BN) * ROWB)
-#define BS(b) (lds + (b) * (BM + BN) * ROWB + BM * ROWB)
+  // buffer b: A tile at lds + b*(BM+BN)*RB, B tile right after it
+  constexpr int RB = tile_rowb<T>();
+#define AS(b) (lds + (b) * (BM + BN) * RB)
+#define BS(b) (lds + (b) * (BM + BN) * RB + BM * RB)
 
   if (gridDim.z > 1) {
     const long z = blockIdx.z;
@@ -302,13 +320,13 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
           v = gn_apply_chunk<T>(v, a.gn_ab + ((long)r_img[i] * a.cin + a_c[i]) * 2, a.gn_silu);
       }
       int row = (tid >> 3) + RPI * i;
-      *reinterpret_cast<uint4*>(AS(buf) + row * ROWB + kc * 16) = v;
+      *reinterpret_cast<uint4*>(AS(buf) + row * RB + (kc ^ chunk_key<T>(row)) * 16) = v;
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       int cid = tid + NT * i;
       int row = cid >> 3, ch = cid & 7;
-      if (row < BN) *reinterpret_cast<uint4*>(BS(buf) + row * ROWB + ch * 16) = breg[i];
+      if (row < BN) *reinterpret_cast<uint4*>(BS(buf) + row * RB + (ch ^ chunk_key<T>(row)) * 16) = breg[i];
     }
   };
 
@@ -321,19 +339,20 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
   const int lrow = lane & 15, lq = lane >> 4;
 
   auto compute = [&](int cur) {
-    const char* Ab = AS(cur) + (wm * WTM + lrow) * ROWB;
-    const char* Bb = BS(cur) + (wn * WTN + lrow) * ROWB;
+    const char* Ab = AS(cur) + (wm * WTM + lrow) * RB;
+    const char* Bb = BS(cur) + (wn * WTN + lrow) * RB;
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        const int so = ((s * 4 + lq) ^ chunk_key<T>(lrow)) * 16;  // swizzled fragment chunk
         if constexpr (TM * TN > 16) {
           // big wave tiles: hold the B fragments, stream A fragments one at a time (register budget)
           bf16x8 bfv[TN];
 #pragma unroll
-          for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROWB + s * 64 + lq * 16);
+          for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * RB + so);
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROWB + s * 64 + lq * 16);
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * RB + so);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
@@ -341,9 +360,9 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
         } else {
           bf16x8 af[TM], bfv[TN];
 #pragma unroll
-          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROWB + s * 64 + lq * 16);
+          for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * RB + so);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROWB + s * 64 + lq * 16);
+          for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * RB + so);
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -356,9 +375,9 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
       for (int s = 0; s < 8; ++s) {
         float af[TM], bfv[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const float*>(Ab + i * 16 * ROWB + (s * 4 + lq) * 4);
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const float*>(Ab + i * 16 * RB + (s * 4 + lq) * 4);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const float*>(Bb + j * 16 * ROWB + (s * 4 + lq) * 4);
+        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const float*>(Bb + j * 16 * RB + (s * 4 + lq) * 4);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -404,7 +423,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 
 #undef AS
 #undef BS
-  if constexpr (sizeof(T) == 2 && TM % 2 == 0 && (BM / 2) * (BN + 4) * 4 <= 2 * (BM + BN) * ROWB) {
+  if constexpr (sizeof(T) == 2 && TM % 2 == 0 && (BM / 2) * (BN + 4) * 4 <= conv_lds_bytes<T, BM, BN>()) {
     if (a.epi_vec && epi_vec_ok(a)) {
       epilogue_vec<BM, BN, WGM, WGN, NT>(acc, a, m0, n0, wm, wn, lane, tid, lds);
       return;
@@ -456,7 +475,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 template <typename T, int BM, int BN, int WGM, int WGN>
 int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
   dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
-  size_t lds = 2 * (BM + BN) * ROWB;
+  size_t lds = conv_lds_bytes<T, BM, BN>();
   if (vec)
     hipLaunchKernelGGL((conv_kernel<T, BM, BN, WGM, WGN, true>), grid, dim3(WGM * WGN * 64), lds, s, a);
   else
@@ -468,7 +487,7 @@ int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
 template <int BM, int BN, int WGM, int WGN>
 int launch_plain(const ConvArgs& a, hipStream_t s) {
   dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
-  size_t lds = 2 * (BM + BN) * ROWB;
+  size_t lds = conv_lds_bytes<bf16, BM, BN>();
   // 2-deep register prefetch where the register budget allows it (<= 8 waves per block)
   constexpr bool PF = (WGM * WGN <= 8);
   if (PF && g_pf2)
@@ -503,414 +522,6 @@ int launch_plain_auto(const ConvArgs& a, hipStream_t s) {
     case 4: return launch_plain<64, 128, 2, 2>(a, s);
     default: return launch_plain<128, 64, 2, 2>(a, s);
   }
-}
-
-// ============================================================================================
-// bf16 main path: LDS-DMA (global_load_lds_dwordx4) staged implicit GEMM with a STAGES-deep
-// ring. Each lane's 16-byte source address is computed per k-tile (the implicit-im2col gather,
-// zero page for padding / tails), so the A operand never passes through VGPRs; the LDS image is
-// lane-linear per wave instruction ([row][8 x 16-byte slots], 128-byte rows) and XOR-swizzled
-// through the SOURCE address (slot s of row r holds k-chunk s ^ (r & 7)), read back with the same
-// XOR so the MFMA fragment reads (ds_read_b128) spread over the banks. Waits are counted
-// (s_waitcnt vmcnt(N) + raw s_barrier), so STAGES-2 tiles stay in flight across each barrier.
-// No GroupNorm prologue here: GN+SiLU inputs are materialised by rdeic_groupnorm_apply first.
-// ============================================================================================
-__device__ uint4 g_zero_page[64];  // 1 KiB of zeros: source of every padded / out-of-range chunk
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int BM, int BN, int WGM, int WGN, int STAGES>
-__global__ __launch_bounds__(WGM * WGN * 64) void conv_glds_kernel(ConvArgs a) {
-  constexpr int NW = WGM * WGN;
-  constexpr int NT = NW * 64;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  constexpr int AI = BM / NW / 8;  // glds instructions per lane per stage (A)
-  constexpr int BI = BN / NW / 8;  // (B)
-  constexpr int PER = AI + BI;
-  constexpr int WTM = BM / WGM, WTN = BN / WGN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave split");
-  static_assert(STAGES >= 2 && STAGES <= 4, "stages");
-
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-
-  if (gridDim.z > 1) {
-    const long z = blockIdx.z;
-    a.in0 += z * a.in_bs * 2; a.in1 += z * a.in_bs * 2;
-    a.weight += z * a.w_bs * 2;
-    a.out += z * a.out_bs * (a.out_f32 ? 4 : 2);
-  }
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int hw_o = a.ho * a.wo;
-  const int hin = a.up2 ? 2 * a.h : a.h, win = a.up2 ? 2 * a.w : a.w;
-  const int lrow8 = lane >> 3;
-  const int g = (lane & 7) ^ lrow8;  // this lane's k-chunk (fixed for all k-tiles and rows)
-  const char* zp = reinterpret_cast<const char*>(g_zero_page);
-
-  int r_img[AI], r_iy[AI], r_ix[AI];
-#pragma unroll
-  for (int j = 0; j < AI; ++j) {
-    const int m = m0 + wave * (BM / NW) + j * 8 + lrow8;
-    if (m < a.M) {
-      int img = m / hw_o, rem = m - img * hw_o;
-      int oy = rem / a.wo, ox = rem - oy * a.wo;
-      r_img[j] = img;
-      r_iy[j] = oy * a.stride - a.pad_t;
-      r_ix[j] = ox * a.stride - a.pad_l;
-    } else {
-      r_img[j] = -1; r_iy[j] = 0; r_ix[j] = 0;
-    }
-  }
-  const char* b_row[BI];
-#pragma unroll
-  for (int j = 0; j < BI; ++j) {
-    const int nn = n0 + wave * (BN / NW) + j * 8 + lrow8;
-    b_row[j] = nn < a.cout ? a.weight + ((long)nn * a.wld + g * 8) * 2 : nullptr;
-  }
-
-  auto issue = [&](int kt, int buf) {
-    char* sb = lds + buf * STAGE;
-    const int k0 = kt * 64 + g * 8;
-    const bool kval = k0 < a.ktot;
-    int tap = kval ? k0 / a.cin : 0;
-    int c = k0 - tap * a.cin;
-    int ky = tap / a.kw, kx = tap - ky * a.kw;
-    const char* base; int ld, cs;
-    if (c < a.c0) { base = a.in0; ld = a.ld0; cs = c; } else { base = a.in1; ld = a.ld1; cs = c - a.c0; }
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-      int iy = r_iy[j] + ky, ix = r_ix[j] + kx;
-      const bool ok = kval && r_img[j] >= 0 && iy >= 0 && iy < hin && ix >= 0 && ix < win;
-      if (a.up2) { iy >>= 1; ix >>= 1; }
-      const char* src = ok ? base + ((((long)r_img[j] * a.h + iy) * a.w + ix) * ld + cs) * 2 : zp;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(sb + (wave * (BM / NW) + j * 8) * 128),
-                                       16, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < BI; ++j) {
-      const char* src = b_row[j] ? b_row[j] + (long)kt * 128 : zp;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)src, (__attribute__((address_space(3))) void*)(sb + A_BYTES + (wave * (BN / NW) + j * 8) * 128),
-          16, 0, 0);
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int lr = lane & 15, lq = lane >> 4;
-  const int nk = a.nk;
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s, s);
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int after = min(STAGES - 2, nk - 1 - kt);  // stages issued after tile kt
-    if constexpr (STAGES >= 4) {
-      if (after >= 2) wait_vmcnt<2 * PER>();
-      else if (after == 1) wait_vmcnt<PER>();
-      else wait_vmcnt<0>();
-    } else if constexpr (STAGES == 3) {
-      if (after >= 1) wait_vmcnt<PER>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-    const char* Ab = lds + (kt % STAGES) * STAGE + (wm * WTM + lr) * 128;
-    const char* Bb = lds + (kt % STAGES) * STAGE + A_BYTES + (wn * WTN + lr) * 128;
-    const int sw = lr & 7;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int slot = ((s * 4 + lq) ^ sw) * 16;
-      bf16x8 af[TM], bfv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * 128 + slot);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * 128 + slot);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  }
-
-  // ---------------- epilogue (same semantics as conv_kernel)
-  if constexpr ((BM / 2) * (BN + 4) * 4 <= STAGES * STAGE) {
-    if (a.epi_vec && epi_vec_ok(a)) {
-      __syncthreads();  // every wave is past its last ds_read of the ring
-      epilogue_vec<BM, BN, WGM, WGN, 512>(acc, a, m0, n0, wm, wn, lane, tid, lds);
-      return;
-    }
-  }
-  const bool of32 = a.out_f32;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
-      if (m >= a.M) continue;
-      const int img = m / hw_o;
-      int oy = 0, ox = 0;
-      if (a.out_mode == 1) { int rem = m - img * hw_o; oy = rem / a.wo; ox = rem - oy * a.wo; }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nn = n0 + wn * WTN + j * 16 + lr;
-        if (nn >= a.cout) continue;
-        float v = acc[i][j][r];
-        if (a.bias) v += a.bias[nn];
-        if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
-        v = apply_act(v, a.act, a.act_param);
-        long oidx, ridx;
-        if (a.out_mode == 1) {
-          int c = nn >> 2, dy = (nn >> 1) & 1, dx = nn & 1;
-          long p = ((long)img * (2 * a.ho) + (2 * oy + dy)) * (2 * a.wo) + (2 * ox + dx);
-          oidx = p * a.out_ld + c;
-          ridx = p * a.res_ld + c;
-        } else {
-          oidx = (long)m * a.out_ld + nn;
-          ridx = (long)m * a.res_ld + nn;
-        }
-        if (a.res) v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const bf16*>(a.res)[ridx]);
-        if (of32) reinterpret_cast<float*>(a.out)[oidx] = v;
-        else reinterpret_cast<bf16*>(a.out)[oidx] = from_f32<bf16>(v);
-      }
-    }
-  }
-}
-
-template <int BM, int BN, int WGM, int WGN, int STAGES>
-int launch_glds(const ConvArgs& a, hipStream_t s) {
-  dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
-  size_t lds = (size_t)STAGES * (BM + BN) * 128;
-  hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WGM, WGN, STAGES>), grid, dim3(WGM * WGN * 64), lds, s, a);
-  return launch_status();
-}
-
-// ============================================================================================
-// bf16 path 3: one workgroup per CU, 8 waves, big tiles (256x256: 2x4 waves of 128x64;
-// 512x128: 4x2 waves of 128x64), BK = 32 (64-byte LDS rows), STAGES-deep LDS-DMA ring for BOTH
-// operands with a counted vmcnt (loads stay in flight across the raw s_barrier; the loop never
-// drains to 0), one barrier per k-step. LDS rows are 64 B = 4 chunks of 16 B; chunk c of row r
-// lives in slot c ^ key(r), key(r) = bit1(r) | bit2(r) << 1, which makes every ds_read_b128
-// lane group of the 16x16x32 fragment read cover all 64 banks exactly once. Since rows handled
-// by one lane differ by multiples of 16, the key is a per-lane constant on both the DMA side
-// (source pre-swizzle) and the read side. Blocks are remapped so each XCD owns a contiguous run
-// of tiles (N fastest): neighbouring M tiles share input halo rows and all N tiles share the A
-// panel in that XCD's L2. The K order is the same as every other path (k ascending, one
-// 16x16x32 MFMA per 32-k step), so results are bit-identical to paths 0-2.
-// ============================================================================================
-__device__ __forceinline__ int ring_key(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1); }
-
-template <int BM, int BN, int WGM, int WGN, int STAGES>
-__global__ __launch_bounds__(512) void conv_ring_kernel(ConvArgs a, int tiles_m, int tiles_n) {
-  constexpr int NW = 8;
-  static_assert(WGM * WGN == NW, "8 waves");
-  constexpr int ROW = 64;                       // bytes per LDS row (32 bf16 of k)
-  constexpr int A_BYTES = BM * ROW, STAGE = (BM + BN) * ROW;
-  constexpr int AI = BM / 128, BI = BN / 128;   // glds per lane per stage (16 rows x 64 B per wave-instr)
-  constexpr int PER = AI + BI;
-  constexpr int WTM = BM / WGM, WTN = BN / WGN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  static_assert(AI >= 1 && BI >= 1 && AI * 128 == BM && BI * 128 == BN, "tile");
-  static_assert(STAGES >= 3 && STAGES <= 5, "stages");
-
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-
-  // XCD-aware bijective remap of the 1-D grid (blocks with equal orig % 8 share an XCD)
-  const int nwg = gridDim.x;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
-  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
-  const int per_z = tiles_m * tiles_n;
-  const int bz = wgid / per_z;
-  const int rem_t = wgid - bz * per_z;
-  const int tile_m = rem_t / tiles_n, tile_n = rem_t - tile_m * tiles_n;
-  if (bz > 0) {
-    a.in0 += (long)bz * a.in_bs * 2; a.in1 += (long)bz * a.in_bs * 2;
-    a.weight += (long)bz * a.w_bs * 2;
-    a.out += (long)bz * a.out_bs * (a.out_f32 ? 4 : 2);
-  }
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int hw_o = a.ho * a.wo;
-  const int hin = a.up2 ? 2 * a.h : a.h, win = a.up2 ? 2 * a.w : a.w;
-  const int lrow = lane >> 2;                          // row within this wave-instruction's 16 rows
-  const int g = (lane & 3) ^ ring_key(lrow);           // k-chunk this lane stages (fixed)
-  const char* zp = reinterpret_cast<const char*>(g_zero_page);
-
-  int r_img[AI], r_iy[AI], r_ix[AI];
-#pragma unroll
-  for (int j = 0; j < AI; ++j) {
-    const int m = m0 + 16 * (j * NW + wave) + lrow;
-    if (m < a.M) {
-      int img = m / hw_o, rem = m - img * hw_o;
-      int oy = rem / a.wo, ox = rem - oy * a.wo;
-      r_img[j] = img;
-      r_iy[j] = oy * a.stride - a.pad_t;
-      r_ix[j] = ox * a.stride - a.pad_l;
-    } else {
-      r_img[j] = -1; r_iy[j] = 0; r_ix[j] = 0;
-    }
-  }
-  const char* b_row[BI];
-#pragma unroll
-  for (int j = 0; j < BI; ++j) {
-    const int nn = n0 + 16 * (j * NW + wave) + lrow;
-    b_row[j] = nn < a.cout ? a.weight + ((long)nn * a.wld + g * 8) * 2 : nullptr;
-  }
-
-  auto issue = [&](int kt, int buf) {
-    char* sb = lds + buf * STAGE;
-    const int k0 = kt * 32 + g * 8;
-    const bool kval = k0 < a.ktot;
-    const int tap = kval ? k0 / a.cin : 0;
-    const int c = k0 - tap * a.cin;
-    const int ky = tap / a.kw, kx = tap - ky * a.kw;
-    const char* base; int ld, cs;
-    if (c < a.c0) { base = a.in0; ld = a.ld0; cs = c; } else { base = a.in1; ld = a.ld1; cs = c - a.c0; }
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-      int iy = r_iy[j] + ky, ix = r_ix[j] + kx;
-      const bool ok = kval && r_img[j] >= 0 && iy >= 0 && iy < hin && ix >= 0 && ix < win;
-      if (a.up2) { iy >>= 1; ix >>= 1; }
-      const char* src = ok ? base + ((((long)r_img[j] * a.h + iy) * a.w + ix) * ld + cs) * 2 : zp;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(sb + 16 * (j * NW + wave) * ROW),
-                                       16, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < BI; ++j) {
-      const char* src = b_row[j] ? b_row[j] + (long)kt * 64 : zp;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)src, (__attribute__((address_space(3))) void*)(sb + A_BYTES + 16 * (j * NW + wave) * ROW),
-          16, 0, 0);
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int lr = lane & 15, lq = lane >> 4;
-  const int slot = (lq ^ ring_key(lr)) * 16;
-  const int nk = (a.ktot + 31) / 32;
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s, s);
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int after = min(STAGES - 2, nk - 1 - kt);  // stages issued after tile kt so far
-    if constexpr (STAGES == 5) {
-      if (after >= 3) wait_vmcnt<3 * PER>();
-      else if (after == 2) wait_vmcnt<2 * PER>();
-      else if (after == 1) wait_vmcnt<PER>();
-      else wait_vmcnt<0>();
-    } else if constexpr (STAGES == 4) {
-      if (after >= 2) wait_vmcnt<2 * PER>();
-      else if (after == 1) wait_vmcnt<PER>();
-      else wait_vmcnt<0>();
-    } else {
-      if (after >= 1) wait_vmcnt<PER>();
-      else wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-    const char* sb = lds + (kt % STAGES) * STAGE;
-    const char* Ab = sb + (wm * WTM + lr) * ROW + slot;
-    const char* Bb = sb + A_BYTES + (wn * WTN + lr) * ROW + slot;
-    bf16x8 bfv[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * ROW);
-    bf16x8 af[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * ROW);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-
-  // ---------------- epilogue (same semantics as conv_kernel)
-  const bool of32 = a.out_f32;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
-      if (m >= a.M) continue;
-      const int img = m / hw_o;
-      int oy = 0, ox = 0;
-      if (a.out_mode == 1) { int rem = m - img * hw_o; oy = rem / a.wo; ox = rem - oy * a.wo; }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nn = n0 + wn * WTN + j * 16 + lr;
-        if (nn >= a.cout) continue;
-        float v = acc[i][j][r];
-        if (a.bias) v += a.bias[nn];
-        if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
-        v = apply_act(v, a.act, a.act_param);
-        long oidx, ridx;
-        if (a.out_mode == 1) {
-          int c = nn >> 2, dy = (nn >> 1) & 1, dx = nn & 1;
-          long p = ((long)img * (2 * a.ho) + (2 * oy + dy)) * (2 * a.wo) + (2 * ox + dx);
-          oidx = p * a.out_ld + c;
-          ridx = p * a.res_ld + c;
-        } else {
-          oidx = (long)m * a.out_ld + nn;
-          ridx = (long)m * a.res_ld + nn;
-        }
-        if (a.res) v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const bf16*>(a.res)[ridx]);
-        if (of32) reinterpret_cast<float*>(a.out)[oidx] = v;
-        else reinterpret_cast<bf16*>(a.out)[oidx] = from_f32<bf16>(v);
-      }
-    }
-  }
-}
-
-template <int BM, int BN, int WGM, int WGN, int STAGES>
-int launch_ring(const ConvArgs& a, hipStream_t s) {
-  const int tm = cdiv(a.M, BM), tn = cdiv(a.cout, BN);
-  const long nwg = (long)tm * tn * a.batch;
-  if (nwg > 0x7fffffffL) return RDEIC_EINVAL;
-  const size_t lds = (size_t)STAGES * (BM + BN) * 64;
-  hipLaunchKernelGGL((conv_ring_kernel<BM, BN, WGM, WGN, STAGES>), dim3((unsigned)nwg), dim3(512), lds, s, a, tm, tn);
-  return launch_status();
-}
-
-// Path 3 tile choice: 256x256 unless cout <= 128 (then 512x128); returns -1 when the shape is
-// better served by the smaller tiles of path 2 (too few tiles to fill the chip).
-int launch_ring_auto(const ConvArgs& a, hipStream_t s) {
-  const long t256 = (long)cdiv(a.M, 256) * cdiv(a.cout, 256) * a.batch;
-  const long t512 = (long)cdiv(a.M, 512) * cdiv(a.cout, 128) * a.batch;
-  const float u256 = (float)a.cout / (cdiv(a.cout, 256) * 256.f);
-  const float u128 = (float)a.cout / (cdiv(a.cout, 128) * 128.f);
-  if (u128 > u256 + 0.01f && t512 >= 256) return launch_ring<512, 128, 4, 2, 4>(a, s);
-  if (t256 >= 256) return launch_ring<256, 256, 2, 4, 4>(a, s);
-  return -1;
 }
 
 // ============================================================================================
@@ -1037,22 +648,11 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
   if (d->c1) vec = vec && (d->c1 % epc == 0) && (d->ld1 % epc == 0) && (((uintptr_t)d->in1) % 16 == 0);
   if (((uintptr_t)d->weight) % 16 != 0) return RDEIC_EINVAL;
 
-  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 1) {
-    // LDS-DMA pipelined path (wld % 64 == 0 and 16-byte aligned rows are guaranteed above)
-    if (d->cout % 128 != 0 && d->cout % 64 == 0) return launch_glds<128, 64, 2, 2, 3>(a, s);
-    if (a.M <= 8192) return launch_glds<64, 128, 2, 2, 3>(a, s);
-    return launch_glds<128, 128, 2, 2, 3>(a, s);
-  }
   if (d->dtype == 1 && vec && d->cout <= 4 && d->c0 % 32 == 0 && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad_t == 1 &&
       d->pad_l == 1 && !d->up2 && !d->c1 && d->out_mode == 0 && a.batch == 1 && d->ho == d->h && d->wo == d->w &&
       g_conv_path != 0)
     return launch_smallc(a, s);
-  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 3) {
-    const int rc = launch_ring_auto(a, s);
-    if (rc != -1) return rc;
-    return launch_plain_auto(a, s);
-  }
-  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path == 2) return launch_plain_auto(a, s);
+  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path != 0) return launch_plain_auto(a, s);
   if (d->dtype == 1) {
     if (d->cout <= 16) return launch_cfg<bf16, 128, 16, 4, 1>(a, vec, s);
     if (d->cout <= 32) return launch_cfg<bf16, 128, 32, 4, 1>(a, vec, s);

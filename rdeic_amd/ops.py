@@ -88,9 +88,9 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
            act: int = NONE, slope: float = 0.0, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False) -> torch.Tensor:
     """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC)."""
-    if gn is not None and _lds_dma_eligible(x, x2, p):
-        # the LDS-DMA conv path has no register stage to apply GroupNorm+SiLU in: materialise the
-        # normalised (concatenated) input once with the vectorised apply kernel instead
+    if gn is not None and _gn_materialize(x, x2, p):
+        # the big-tile conv path has no GroupNorm prologue (it is VALU-bound there): materialise the
+        # normalised (concatenated) input once with the vectorised, HBM-rate apply kernel instead
         xin = torch.empty(x.shape[:3] + (p.cin,), dtype=x.dtype, device=x.device)
         c0 = x.shape[3]
         group_norm_apply(x, gn, gn_silu, out=xin[..., :c0])
@@ -200,7 +200,7 @@ def conv_profile_breakdown(records):
     return out
 
 
-CONV_PATH = 2  # mirrors rdeic_set_conv_path (0 fused-GN 128-tiles, 1 LDS-DMA ring, 2 big register-staged tiles)
+CONV_PATH = 2  # mirrors rdeic_set_conv_path (0: fused-GN 128-tiles everywhere, 2: big-tile auto choice)
 
 
 def set_conv_path(path: int) -> int:
@@ -212,12 +212,12 @@ def set_conv_path(path: int) -> int:
 
 
 def set_conv_option(key: int, value: int) -> int:
-    """rdeic_set_conv_option: key 0 = vectorised LDS-staged epilogue (1 on, 0 off)."""
+    """rdeic_set_conv_option: key 0 vectorised epilogue, 1 dh=64 attention kernel, 2 two-deep prefetch."""
     return int(_lib.load().rdeic_set_conv_option(int(key), int(value)))
 
 
-def _lds_dma_eligible(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) -> bool:
-    """Same rule as rdeic_conv2d's dispatch to conv_glds_kernel (bf16, 16-byte gathers, cout > 32)."""
+def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) -> bool:
+    """Same rule as rdeic_conv2d's dispatch to the big-tile path (bf16, 16-byte gathers, cout > 32)."""
     if CONV_PATH == 0 or x.dtype != torch.bfloat16 or p.cout <= 32:
         return False
     for t in (x, x2):
