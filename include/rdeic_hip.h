@@ -79,7 +79,8 @@ int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
 int rdeic_set_conv_path(int32_t path);
 /* Tuning switches (process-wide). key 0: LDS-staged vector epilogue on (1, default) / off (0);
  * key 1: transposed head-dim-64 attention kernel on (1, default) / off (0);
- * key 2: two-deep register prefetch in the register-staged conv path (0 default, 1 on).
+ * key 2: two-deep register prefetch in the register-staged conv path (0 default, 1 on);
+ * key 3: XOR-swizzled 128-byte LDS rows on the <= 8-wave conv tiles (1 default) / padded rows (0).
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way. */
 int rdeic_set_conv_option(int32_t key, int32_t value);
 

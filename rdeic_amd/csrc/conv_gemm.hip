@@ -44,6 +44,7 @@ struct ConvArgs {
 
 int g_conv_path = 2;  // 0: 128-tiles with the fused GroupNorm prologue only, 2 (default): big-tile auto choice
 int g_epi_vec = 1;    // LDS-staged vector epilogue (rdeic_set_conv_option(0, v))
+int g_swz = 1;        // swizzled 128-B LDS rows where they win (1) / padded 144-B rows everywhere (0) (option 3)
 int g_pf2 = 0;        // 2-deep register prefetch in the plain path (rdeic_set_conv_option(2, v)); measured neutral, off
 
 constexpr int ROWB = 144;  // fp32 tiles: LDS bytes per row, 128 B of k-data + 16 B pad (bank spread)
@@ -53,15 +54,15 @@ constexpr int ROWB = 144;  // fp32 tiles: LDS bytes per row, 128 B of k-data + 1
 // fragment reads (rows r..r+15, one chunk column) then covers all 64 banks once, and a row's
 // 8 chunks written by 8 lanes still cover 32 banks. Rows a lane touches differ by multiples of
 // 16, so key(r) is a per-lane constant on both sides.
-template <typename T> __host__ __device__ constexpr int tile_rowb() { return sizeof(T) == 2 ? 128 : ROWB; }
-template <typename T> __device__ __forceinline__ int chunk_key(int r) {
-  if constexpr (sizeof(T) == 2) return (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2);
+template <typename T, bool SWZ = true> __host__ __device__ constexpr int tile_rowb() { return (sizeof(T) == 2 && SWZ) ? 128 : ROWB; }
+template <typename T, bool SWZ = true> __device__ __forceinline__ int chunk_key(int r) {
+  if constexpr (sizeof(T) == 2 && SWZ) return (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2);
   return 0;
 }
 // dynamic LDS of conv_kernel: the double-buffered tiles, or the vector epilogue's half tile
-template <typename T, int BM, int BN> __host__ __device__ constexpr int conv_lds_bytes() {
-  return (2 * (BM + BN) * tile_rowb<T>() > (BM / 2) * (BN + 4) * 4 || sizeof(T) != 2)
-             ? 2 * (BM + BN) * tile_rowb<T>()
+template <typename T, int BM, int BN, bool SWZ = true> __host__ __device__ constexpr int conv_lds_bytes() {
+  return (2 * (BM + BN) * tile_rowb<T, SWZ>() > (BM / 2) * (BN + 4) * 4 || sizeof(T) != 2)
+             ? 2 * (BM + BN) * tile_rowb<T, SWZ>()
              : (BM / 2) * (BN + 4) * 4;
 }
 
@@ -187,7 +188,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
 }
 
 // GNP: compile the GroupNorm+SiLU gather prologue in (false = plain gather, fewer VGPRs / VALU).
-template <typename T, int BM, int BN, int WGM, int WGN, bool VEC, bool GNP = true, bool PF2 = false>
+template <typename T, int BM, int BN, int WGM, int WGN, bool VEC, bool GNP = true, bool PF2 = false, bool SWZ = true>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int BK = MmaTraits<T>::BK;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // buffer b: A tile at lds + b*(BM+BN)*RB, B tile right after it
-  constexpr int RB = tile_rowb<T>();
+  constexpr int RB = tile_rowb<T, SWZ>();
 #define AS(b) (lds + (b) * (BM + BN) * RB)
 #define BS(b) (lds + (b) * (BM + BN) * RB + BM * RB)
 
@@ -320,13 +321,13 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
           v = gn_apply_chunk<T>(v, a.gn_ab + ((long)r_img[i] * a.cin + a_c[i]) * 2, a.gn_silu);
       }
       int row = (tid >> 3) + RPI * i;
-      *reinterpret_cast<uint4*>(AS(buf) + row * RB + (kc ^ chunk_key<T>(row)) * 16) = v;
+      *reinterpret_cast<uint4*>(AS(buf) + row * RB + (kc ^ chunk_key<T, SWZ>(row)) * 16) = v;
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       int cid = tid + NT * i;
       int row = cid >> 3, ch = cid & 7;
-      if (row < BN) *reinterpret_cast<uint4*>(BS(buf) + row * RB + (ch ^ chunk_key<T>(row)) * 16) = breg[i];
+      if (row < BN) *reinterpret_cast<uint4*>(BS(buf) + row * RB + (ch ^ chunk_key<T, SWZ>(row)) * 16) = breg[i];
     }
   };
 
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int so = ((s * 4 + lq) ^ chunk_key<T>(lrow)) * 16;  // swizzled fragment chunk
+        const int so = ((s * 4 + lq) ^ chunk_key<T, SWZ>(lrow)) * 16;  // swizzled fragment chunk
         if constexpr (TM * TN > 16) {
           // big wave tiles: hold the B fragments, stream A fragments one at a time (register budget)
           bf16x8 bfv[TN];
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 
 #undef AS
 #undef BS
-  if constexpr (sizeof(T) == 2 && TM % 2 == 0 && (BM / 2) * (BN + 4) * 4 <= conv_lds_bytes<T, BM, BN>()) {
+  if constexpr (sizeof(T) == 2 && TM % 2 == 0 && (BM / 2) * (BN + 4) * 4 <= conv_lds_bytes<T, BM, BN, SWZ>()) {
     if (a.epi_vec && epi_vec_ok(a)) {
       epilogue_vec<BM, BN, WGM, WGN, NT>(acc, a, m0, n0, wm, wn, lane, tid, lds);
       return;
@@ -487,6 +488,16 @@ int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
 template <int BM, int BN, int WGM, int WGN>
 int launch_plain(const ConvArgs& a, hipStream_t s) {
   dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
+  // measured A/B (one process, bit-identical results): the swizzled 128-B rows win on the
+  // 4- and 8-wave tiles (+3-6 %) and lose on the 16-wave 256x256 tile (-16 %), which keeps the
+  // padded 144-B rows
+  constexpr bool SWZ_OK = (WGM * WGN <= 8);
+  if (!g_swz || !SWZ_OK) {
+    constexpr int lds0 = conv_lds_bytes<bf16, BM, BN, false>();
+    hipLaunchKernelGGL((conv_kernel<bf16, BM, BN, WGM, WGN, true, false, false, false>), grid, dim3(WGM * WGN * 64),
+                       lds0, s, a);
+    return launch_status();
+  }
   size_t lds = conv_lds_bytes<bf16, BM, BN>();
   // 2-deep register prefetch where the register budget allows it (<= 8 waves per block)
   constexpr bool PF = (WGM * WGN <= 8);
@@ -677,5 +688,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 0) { int prev = g_epi_vec; g_epi_vec = value; return prev; }
   if (key == 1) { int prev = rdeic_g_attn64; rdeic_g_attn64 = value; return prev; }
   if (key == 2) { int prev = g_pf2; g_pf2 = value; return prev; }
+  if (key == 3) { int prev = g_swz; g_swz = value; return prev; }
   return RDEIC_EINVAL;
 }
