@@ -72,6 +72,12 @@ typedef struct rdeic_conv_desc {
 } rdeic_conv_desc;
 
 int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
+/* Split-K variant for small-M / large-K layers (the UNet's 8x8 and 16x16 levels): `splits`
+ * k-ranges accumulate into the caller's fp32 workspace (>= splits * n*ho*wo * cout floats), then a
+ * reduction sums them in split order (deterministic) and applies bias / emb / act / residual.
+ * bf16 only, no GN prologue, out_mode 0, batch 1, cout % 8 == 0. Not bit-identical to
+ * rdeic_conv2d (different k grouping): not for the entropy-model nets. */
+int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats, void* stream);
 /* 2 (default): bf16 convs without a GN prologue pick among the big register-staged tiles
  * (256x256 / 256x128 / 128x256 / 128x128 / 64x128 / 128x64); 0: the 128-tile kernel with the
  * fused GroupNorm prologue everywhere (A/B timing, debugging). Results are bit-identical.

@@ -40,6 +40,7 @@ struct ConvArgs {
   long in_bs, w_bs, out_bs;  // batched-GEMM strides (elements), blockIdx.z
   int batch;
   int epi_vec;               // 1: LDS-staged vector epilogue where eligible
+  int splits, kper;          // split-K: blockIdx.z = split, k-steps [z*kper, (z+1)*kper), raw fp32 partial out
 };
 
 int g_conv_path = 2;  // 0: 128-tiles with the fused GroupNorm prologue only, 2 (default): big-tile auto choice
@@ -207,7 +208,13 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 #define AS(b) (lds + (b) * (BM + BN) * RB)
 #define BS(b) (lds + (b) * (BM + BN) * RB + BM * RB)
 
-  if (gridDim.z > 1) {
+  int kt_begin = 0, kt_end = a.nk;
+  if (a.splits > 1) {
+    const int z = blockIdx.z;
+    kt_begin = min(a.nk, z * a.kper);
+    kt_end = min(a.nk, kt_begin + a.kper);
+    a.out += (long)z * a.M * a.out_ld * 4;  // this split's fp32 partial slab
+  } else if (gridDim.z > 1) {
     const long z = blockIdx.z;
     a.in0 += z * a.in_bs * ES; a.in1 += z * a.in_bs * ES;
     a.weight += z * a.w_bs * ES;
@@ -409,15 +416,17 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
     }
     if (kt < a.nk) compute(0);
   } else {
-    gather_a(0, areg);
-    gather_b(0, breg);
-    store_tiles(0, areg, breg);
+    if (kt_begin < kt_end) {
+      gather_a(kt_begin, areg);
+      gather_b(kt_begin, breg);
+      store_tiles(0, areg, breg);
+    }
     __syncthreads();
-    for (int kt = 0; kt < a.nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < a.nk) { gather_a(kt + 1, areg); gather_b(kt + 1, breg); }
+    for (int kt = kt_begin; kt < kt_end; ++kt) {
+      const int cur = (kt - kt_begin) & 1;
+      if (kt + 1 < kt_end) { gather_a(kt + 1, areg); gather_b(kt + 1, breg); }
       compute(cur);
-      if (kt + 1 < a.nk) store_tiles(cur ^ 1, areg, breg);
+      if (kt + 1 < kt_end) store_tiles(cur ^ 1, areg, breg);
       __syncthreads();
     }
   }
@@ -621,15 +630,56 @@ int launch_smallc(const ConvArgs& a, hipStream_t s) {
   return launch_status();
 }
 
+// Deterministic split-K reduction + epilogue: out = act(sum_z part[z] + bias + emb) + res, the
+// splits summed in index order in fp32 (8 channels per thread, 16-byte loads / stores).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, const float* __restrict__ part) {
+  const int cp = a.cout >> 3;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)a.M * cp) return;
+  const int m = (int)(i / cp), nn = (int)(i - (long)m * cp) * 8;
+  const long slab = (long)a.M * a.cout;
+  float v[8];
+  {
+    const float4 x0 = *reinterpret_cast<const float4*>(part + (long)m * a.cout + nn);
+    const float4 x1 = *reinterpret_cast<const float4*>(part + (long)m * a.cout + nn + 4);
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+  }
+  for (int z = 1; z < a.splits; ++z) {
+    const float* pz = part + z * slab + (long)m * a.cout + nn;
+    const float4 x0 = *reinterpret_cast<const float4*>(pz), x1 = *reinterpret_cast<const float4*>(pz + 4);
+    v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w; v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+  }
+  const int hw_o = a.ho * a.wo;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if (a.bias) v[e] += a.bias[nn + e];
+    if (a.emb) v[e] += a.emb[(long)(m / hw_o) * a.emb_ld + nn + e];
+    v[e] = apply_act(v[e], a.act, a.act_param);
+    if (a.res) v[e] += a.out_f32 ? reinterpret_cast<const float*>(a.res)[(long)m * a.res_ld + nn + e]
+                                 : to_f32(reinterpret_cast<const bf16*>(a.res)[(long)m * a.res_ld + nn + e]);
+  }
+  if (a.out_f32) {
+    float* o = reinterpret_cast<float*>(a.out) + (long)m * a.out_ld + nn;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = v[e];
+  } else {
+    bf16 ov[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ov[e] = from_f32<bf16>(v[e]);
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + nn) = *reinterpret_cast<uint4*>(ov);
+  }
+}
+
 }  // namespace
 
-extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
+namespace {
+// descriptor -> kernel arguments (validation shared by rdeic_conv2d / rdeic_conv2d_splitk)
+int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec) {
   if (!d || !d->in0 || !d->weight || !d->out) return RDEIC_EINVAL;
   if (d->c0 <= 0 || d->c1 < 0 || (d->c1 > 0 && !d->in1) || d->cout <= 0 || d->kh <= 0 || d->kw <= 0 ||
       d->stride <= 0 || d->n <= 0 || d->ho <= 0 || d->wo <= 0)
     return RDEIC_EINVAL;
   if (d->dtype != 0 && d->dtype != 1) return RDEIC_EINVAL;
-  ConvArgs a;
   a.in0 = (const char*)d->in0; a.in1 = (const char*)(d->in1 ? d->in1 : d->in0);
   a.c0 = d->c0; a.c1 = d->c1; a.ld0 = d->ld0; a.ld1 = d->c1 ? d->ld1 : d->ld0;
   a.n = d->n; a.h = d->h; a.w = d->w; a.up2 = d->up2;
@@ -643,6 +693,7 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
   a.out = (char*)d->out; a.out_ld = d->out_ld; a.out_mode = d->out_mode;
   a.out_f32 = d->out_f32;
   a.epi_vec = g_epi_vec;
+  a.splits = 1; a.kper = 0;
   a.M = d->n * d->ho * d->wo;
   a.batch = d->batch > 1 ? d->batch : 1;
   a.in_bs = d->in_bs; a.w_bs = d->w_bs; a.out_bs = d->out_bs;
@@ -653,11 +704,20 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
   if (d->wld < a.ktot || d->wld % 64 != 0) return RDEIC_EINVAL;
   a.nk = (a.ktot + BK - 1) / BK;
   if (d->out_mode == 1 && (d->cout % 4 != 0)) return RDEIC_EINVAL;
-  hipStream_t s = (hipStream_t)stream;
   const int epc = d->dtype == 1 ? 8 : 4;
-  bool vec = (d->c0 % epc == 0) && (d->ld0 % epc == 0) && (((uintptr_t)d->in0) % 16 == 0);
+  vec = (d->c0 % epc == 0) && (d->ld0 % epc == 0) && (((uintptr_t)d->in0) % 16 == 0);
   if (d->c1) vec = vec && (d->c1 % epc == 0) && (d->ld1 % epc == 0) && (((uintptr_t)d->in1) % 16 == 0);
   if (((uintptr_t)d->weight) % 16 != 0) return RDEIC_EINVAL;
+  return RDEIC_OK;
+}
+}  // namespace
+
+extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
+  ConvArgs a;
+  bool vec = false;
+  const int rc = make_args(d, a, vec);
+  if (rc != RDEIC_OK) return rc;
+  hipStream_t s = (hipStream_t)stream;
 
   if (d->dtype == 1 && vec && d->cout <= 4 && d->c0 % 32 == 0 && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad_t == 1 &&
       d->pad_l == 1 && !d->up2 && !d->c1 && d->out_mode == 0 && a.batch == 1 && d->ho == d->h && d->wo == d->w &&
@@ -674,6 +734,37 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
     if (d->cout <= 16) return launch_cfg<float, 64, 16, 4, 1>(a, vec, s);
     return launch_cfg<float, 64, 64, 2, 2>(a, vec, s);
   }
+}
+
+// Split-K variant (small-M, large-K layers): `splits` k-ranges computed into a caller-provided
+// fp32 workspace of splits * M * cout floats, then reduced in split order (deterministic) with
+// the bias / emb / activation / residual epilogue. bf16, 16-byte gathers, no GN prologue,
+// out_mode 0, batch 1, cout % 8 == 0. The k-order differs from rdeic_conv2d (not bit-identical
+// to it), so callers that need batch invariance must not use it.
+extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats,
+                                   void* stream) {
+  ConvArgs a;
+  bool vec = false;
+  const int rc = make_args(d, a, vec);
+  if (rc != RDEIC_OK) return rc;
+  if (d->dtype != 1 || !vec || d->gn_ab || d->out_mode != 0 || a.batch != 1 || d->cout % 8 || splits < 2 || !ws ||
+      (d->out_ld % 8) || ((uintptr_t)d->out % 16) || ((uintptr_t)ws % 16))
+    return RDEIC_EINVAL;
+  if (ws_floats < (size_t)splits * a.M * a.cout) return RDEIC_ENOSPC;
+  hipStream_t s = (hipStream_t)stream;
+  ConvArgs p = a;  // partial pass: raw sums into the workspace
+  p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr;
+  p.out = (char*)ws; p.out_ld = a.cout; p.out_f32 = 1;
+  p.splits = splits;
+  p.kper = (a.nk + splits - 1) / splits;
+  dim3 grid(cdiv(a.M, 128), cdiv(a.cout, 128), splits);
+  constexpr int lds = conv_lds_bytes<bf16, 128, 128>();
+  hipLaunchKernelGGL((conv_kernel<bf16, 128, 128, 2, 2, true, false, false, true>), grid, dim3(256), lds, s, p);
+  a.splits = splits;
+  const long chunks = (long)a.M * (a.cout / 8);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, a,
+                     (const float*)ws);
+  return launch_status();
 }
 
 extern "C" int rdeic_set_conv_path(int32_t path) {

@@ -157,18 +157,67 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     d.out_f32 = int(odt == torch.float32 and x.dtype != torch.float32)
     d.batch = 1
     flops = 2.0 * n * ho * wo * p.cout * p.kh * p.kw * p.cin
+    splits = _splitk_count(x, x2, n * ho * wo, p, gn is not None or pixel_shuffle, out)
+
+    def launch():
+        if splits > 1:
+            ws = _splitk_workspace(splits * n * ho * wo * p.cout, x.device)
+            call("rdeic_conv2d_splitk", C.byref(d), splits, ws.data_ptr(), ws.numel(), stream_ptr())
+        else:
+            call("rdeic_conv2d", C.byref(d), stream_ptr())
+
     prof = PROFILE
     if prof is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-        call("rdeic_conv2d", C.byref(d), stream_ptr())
+        launch()
         ev1.record()
         prof.append((flops, ev0, ev1, x.dtype,
                      (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), int(pixel_shuffle))))
     else:
-        call("rdeic_conv2d", C.byref(d), stream_ptr())
+        launch()
     return out
+
+
+# Split-K is opt-in (see splitk_allowed): it changes the k grouping, so layers whose outputs must
+# be batch-invariant (the entropy-model nets) never use it.
+SPLITK_ALLOWED = False
+_SPLITK_WS: dict = {}
+
+
+class splitk_allowed:
+    """Context manager enabling split-K for small-M / large-K convs (UNet / control forward)."""
+
+    def __enter__(self):
+        global SPLITK_ALLOWED
+        self._prev, SPLITK_ALLOWED = SPLITK_ALLOWED, True
+
+    def __exit__(self, *exc):
+        global SPLITK_ALLOWED
+        SPLITK_ALLOWED = self._prev
+
+
+def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor) -> int:
+    """Number of k-splits (1 = none): only when the 128x128 tile grid cannot fill the chip."""
+    if not SPLITK_ALLOWED or fused or x.dtype != torch.bfloat16 or p.cout % 8 or pix_ld(out) % 8:
+        return 1
+    for t in (x, x2):
+        if t is not None and (t.shape[3] % 8 or pix_ld(t) % 8 or t.data_ptr() % 16):
+            return 1
+    tiles = -(-M // 128) * -(-p.cout // 128)
+    nk = -(-(p.kh * p.kw * p.cin) // 64)
+    if tiles >= 192 or nk < 32:
+        return 1
+    return max(1, min(-(-512 // tiles), nk // 16, 8))
+
+
+def _splitk_workspace(n: int, device) -> torch.Tensor:
+    buf = _SPLITK_WS.get(device)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(n, dtype=torch.float32, device=device)
+        _SPLITK_WS[device] = buf
+    return buf
 
 
 # When set to a list, every rdeic_conv2d launch appends (algorithmic FLOPs, start event, end

@@ -304,6 +304,11 @@ class NoiseEstimator:
         return out
 
     def forward(self, x: torch.Tensor, hint: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
+        # the UNet / control convs need no batch invariance: let small-M, large-K layers split K
+        with ops.splitk_allowed():
+            return self._forward(x, hint, t, ctx)
+
+    def _forward(self, x: torch.Tensor, hint: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
         """x: fp32 NHWC [B,h,w,4] latent; hint: NHWC [B,h,w,256] (compute dtype);
         t: int64 [B]; ctx: [Bc,77,1024] (compute dtype, Bc in {1, B}). Returns eps fp32 NHWC."""
         s = self.store

@@ -237,3 +237,28 @@ def test_conv_small_cout_gn(gpu, cout, h, w):
     p = ops.ConvParams.pack(wt, b, pad=1, dtype=torch.bfloat16)
     out = ops.conv2d(xd, p, gn=ab, gn_silu=True, out_f32=True)
     torch.testing.assert_close(_nchw(out), ref, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("cin,cout,hw,res", [(1280, 1280, 8, True), (2560, 1280, 8, False), (640, 640, 16, True)])
+def test_conv_splitk(gpu, cin, cout, hw, res):
+    """Split-K conv (UNet 8x8 / 16x16 levels) vs the fp32 torch reference, with emb + act + residual."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(cin + hw)
+    B = 16
+    x = torch.randn(B, cin, hw, hw, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    b = torch.randn(cout, generator=g)
+    emb = torch.randn(B, cout, generator=g)
+    r = torch.randn(B, cout, hw, hw, generator=g)
+    xq, wq, rq = x.to(torch.bfloat16).float(), w.to(torch.bfloat16).float(), r.to(torch.bfloat16).float()
+    ref = F.silu(F.conv2d(xq, wq, b, padding=1) + emb[:, :, None, None])
+    if res:
+        ref = ref + rq
+    p = ops.ConvParams.pack(w, b, pad=1, dtype=torch.bfloat16)
+    xd, rd = _nhwc(x.to(torch.bfloat16)), _nhwc(r.to(torch.bfloat16))
+    with ops.splitk_allowed():
+        assert ops._splitk_count(xd, None, B * hw * hw, p, False, rd) > 1
+        out = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
+    torch.testing.assert_close(_nchw(out), ref, rtol=2e-2, atol=3e-2)
+    out_plain = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
+    assert (out.float() - out_plain.float()).abs().max().item() < 0.1

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--epi", default="1", help="comma list of epilogue modes to A/B (1 vector, 0 scalar)")
     ap.add_argument("--pf2", default="0", help="comma list of register-prefetch modes to A/B (1 two-deep, 0 one)")
     ap.add_argument("--swz", default="1", help="comma list of LDS layouts to A/B (1 swizzled, 0 padded)")
+    ap.add_argument("--splitk", default="0", help="comma list: 1 = allow split-K (UNet mode)")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []
@@ -56,8 +57,8 @@ def main():
         w = torch.randn(cout, cin, k, k, device="cuda") / math.sqrt(cin * k * k)
         p = ops.ConvParams.pack(w, torch.randn(cout, device="cuda"), stride=stride, pad=k // 2)
         res_t = torch.randn(B, H // stride, W // stride, cout, device="cuda").to(torch.bfloat16)
-        paths = [(int(v), int(e), int(f), int(z)) for v in args.paths.split(",") for e in args.epi.split(",")
-                 for f in args.pf2.split(",") for z in args.swz.split(",")]
+        paths = [(int(v), int(e), int(f), int(z), int(k)) for v in args.paths.split(",") for e in args.epi.split(",")
+                 for f in args.pf2.split(",") for z in args.swz.split(",") for k in args.splitk.split(",")]
         outs = {}
         times = {q: [] for q in paths}
         fn = lambda: ops.conv2d(x, p, res=res_t, act=ops.SILU)  # noqa: E731
@@ -66,6 +67,7 @@ def main():
             ops.set_conv_option(0, q[1])
             ops.set_conv_option(2, q[2])
             ops.set_conv_option(3, q[3])
+            ops.SPLITK_ALLOWED = bool(q[4])
             outs[q] = fn()
         for _ in range(3):
             for q in paths:
@@ -73,18 +75,22 @@ def main():
                 ops.set_conv_option(0, q[1])
                 ops.set_conv_option(2, q[2])
                 ops.set_conv_option(3, q[3])
+                ops.SPLITK_ALLOWED = bool(q[4])
                 times[q].append(bench(fn, args.reps))
         flops = 2.0 * B * (H // stride) * (W // stride) * cout * cin * k * k
         r = dict(name=name)
         for q in paths:
-            r["tf_" + "".join(f"{k}{v}" for k, v in zip("pefz", q))] = round(flops / min(times[q]) / 1e12, 1)
-        r["identical"] = all(torch.equal(outs[paths[0]], outs[q]) for q in paths)
+            r["tf_" + "".join(f"{k}{v}" for k, v in zip("pefzk", q))] = round(flops / min(times[q]) / 1e12, 1)
+        r["identical"] = all(torch.equal(outs[paths[0]], outs[q]) for q in paths if q[4] == 0)
+        r["max_diff_splitk"] = max([(outs[paths[0]].float() - outs[q].float()).abs().max().item()
+                                    for q in paths if q[4] == 1] or [0.0])
         print(json.dumps(r), flush=True)
         res.append(r)
     ops.set_conv_path(2)
     ops.set_conv_option(0, 1)
     ops.set_conv_option(2, 0)
     ops.set_conv_option(3, 1)
+    ops.SPLITK_ALLOWED = False
 
 
 if __name__ == "__main__":
