@@ -72,6 +72,10 @@ typedef struct rdeic_conv_desc {
 } rdeic_conv_desc;
 
 int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
+/* rdeic_conv2d with an explicit tile for the big-tile path (0 256x256/16 waves, 1 256x128/8,
+ * 2 128x256/8, 3 128x128/4, 4 64x128/4, 6 256x128/16, 7 128x256/16, 8 128x128/8, 9 128x128/16,
+ * 10 64x128/8; -1 heuristic). All tiles give bit-identical results, so a caller may autotune. */
+int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream);
 /* Split-K variant for small-M / large-K layers (the UNet's 8x8 and 16x16 levels): `splits`
  * k-ranges accumulate into the caller's fp32 workspace (>= splits * n*ho*wo * cout floats), then a
  * reduction sums them in split order (deterministic) and applies bias / emb / act / residual.
@@ -86,7 +90,9 @@ int rdeic_set_conv_path(int32_t path);
 /* Tuning switches (process-wide). key 0: LDS-staged vector epilogue on (1, default) / off (0);
  * key 1: transposed head-dim-64 attention kernel on (1, default) / off (0);
  * key 2: two-deep register prefetch in the register-staged conv path (0 default, 1 on);
- * key 3: XOR-swizzled 128-byte LDS rows on the <= 8-wave conv tiles (1 default) / padded rows (0).
+ * key 3: XOR-swizzled 128-byte LDS rows on the <= 8-wave conv tiles (1 default) / padded rows (0);
+ * key 4: force the big-tile candidate (0 256x256, 1 256x128, 2 128x256, 3 128x128, 4 64x128,
+ *        5 128x64; -1 = automatic choice, default) — tuning only.
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way. */
 int rdeic_set_conv_option(int32_t key, int32_t value);
 

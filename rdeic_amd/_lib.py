@@ -57,6 +57,7 @@ PROTOTYPES = {
     "rdeic_abi_count": (C.c_int, []),
     "rdeic_conv2d": (C.c_int, [C.POINTER(ConvDesc), _p]),
     "rdeic_conv2d_splitk": (C.c_int, [C.POINTER(ConvDesc), _i32, _p, C.c_size_t, _p]),
+    "rdeic_conv2d_tile": (C.c_int, [C.POINTER(ConvDesc), _i32, _p]),
     "rdeic_groupnorm_ws_floats": (_sz, [_i32, _i32, _i32]),
     "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p,
                                         _i32, _p]),

@@ -46,6 +46,7 @@ struct ConvArgs {
 int g_conv_path = 2;  // 0: 128-tiles with the fused GroupNorm prologue only, 2 (default): big-tile auto choice
 int g_epi_vec = 1;    // LDS-staged vector epilogue (rdeic_set_conv_option(0, v))
 int g_swz = 1;        // swizzled 128-B LDS rows where they win (1) / padded 144-B rows everywhere (0) (option 3)
+int g_force_tile = -1;  // >= 0: force launch_plain_auto's candidate (rdeic_set_conv_option(4, i)), tuning only
 int g_pf2 = 0;        // 2-deep register prefetch in the plain path (rdeic_set_conv_option(2, v)); measured neutral, off
 
 constexpr int ROWB = 144;  // fp32 tiles: LDS bytes per row, 128 B of k-data + 16 B pad (bank spread)
@@ -520,7 +521,7 @@ int launch_plain(const ConvArgs& a, hipStream_t s) {
 
 // Tile choice for the plain path: maximise (useful fraction of the padded tile grid) x (CU fill)
 // x (operand reuse of the tile); the accumulation order does not depend on the choice.
-int launch_plain_auto(const ConvArgs& a, hipStream_t s) {
+int launch_plain_auto(const ConvArgs& a, hipStream_t s, int tile = -1) {
   struct Cand { int bm, bn; float reuse; };
   const Cand cands[] = {{256, 256, 1.0f}, {256, 128, 0.86f}, {128, 256, 0.86f}, {128, 128, 0.72f}, {64, 128, 0.55f},
                         {128, 64, 0.55f}};
@@ -534,12 +535,19 @@ int launch_plain_auto(const ConvArgs& a, hipStream_t s) {
     const float score = useful * fill * cands[i].reuse;
     if (score > best_score + 1e-6f) { best_score = score; best = i; }
   }
+  if (g_force_tile >= 0 && g_force_tile < 11) best = g_force_tile;
+  if (tile >= 0 && tile < 11 && tile != 5) best = tile;
   switch (best) {
     case 0: return launch_plain<256, 256, 4, 4>(a, s);
     case 1: return launch_plain<256, 128, 4, 2>(a, s);
     case 2: return launch_plain<128, 256, 2, 4>(a, s);
     case 3: return launch_plain<128, 128, 2, 2>(a, s);
     case 4: return launch_plain<64, 128, 2, 2>(a, s);
+    case 6: return launch_plain<256, 128, 4, 4>(a, s);
+    case 7: return launch_plain<128, 256, 4, 4>(a, s);
+    case 8: return launch_plain<128, 128, 2, 4>(a, s);
+    case 9: return launch_plain<128, 128, 4, 4>(a, s);
+    case 10: return launch_plain<64, 128, 2, 4>(a, s);
     default: return launch_plain<128, 64, 2, 2>(a, s);
   }
 }
@@ -736,6 +744,19 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
   }
 }
 
+// Explicit tile choice for the big-tile path (autotuning by the caller; every tile gives
+// bit-identical results). tile -1 = the built-in heuristic. Shapes outside the big-tile path
+// (GN prologue, cout <= 32, fp32, unaligned) ignore it and run exactly as rdeic_conv2d.
+extern "C" int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream) {
+  ConvArgs a;
+  bool vec = false;
+  const int rc = make_args(d, a, vec);
+  if (rc != RDEIC_OK) return rc;
+  if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path != 0)
+    return launch_plain_auto(a, (hipStream_t)stream, tile);
+  return rdeic_conv2d(d, stream);
+}
+
 // Split-K variant (small-M, large-K layers): `splits` k-ranges computed into a caller-provided
 // fp32 workspace of splits * M * cout floats, then reduced in split order (deterministic) with
 // the bias / emb / activation / residual epilogue. bf16, 16-byte gathers, no GN prologue,
@@ -780,5 +801,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 1) { int prev = rdeic_g_attn64; rdeic_g_attn64 = value; return prev; }
   if (key == 2) { int prev = g_pf2; g_pf2 = value; return prev; }
   if (key == 3) { int prev = g_swz; g_swz = value; return prev; }
+  if (key == 4) { int prev = g_force_tile; g_force_tile = value; return prev; }
   return RDEIC_EINVAL;
 }

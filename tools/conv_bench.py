@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--pf2", default="0", help="comma list of register-prefetch modes to A/B (1 two-deep, 0 one)")
     ap.add_argument("--swz", default="1", help="comma list of LDS layouts to A/B (1 swizzled, 0 padded)")
     ap.add_argument("--splitk", default="0", help="comma list: 1 = allow split-K (UNet mode)")
+    ap.add_argument("--tiles", default="-1", help="comma list of forced tile candidates (-1 auto, 0..5)")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []
@@ -57,8 +58,9 @@ def main():
         w = torch.randn(cout, cin, k, k, device="cuda") / math.sqrt(cin * k * k)
         p = ops.ConvParams.pack(w, torch.randn(cout, device="cuda"), stride=stride, pad=k // 2)
         res_t = torch.randn(B, H // stride, W // stride, cout, device="cuda").to(torch.bfloat16)
-        paths = [(int(v), int(e), int(f), int(z), int(k)) for v in args.paths.split(",") for e in args.epi.split(",")
-                 for f in args.pf2.split(",") for z in args.swz.split(",") for k in args.splitk.split(",")]
+        paths = [(int(v), int(e), int(f), int(z), int(k), int(t)) for v in args.paths.split(",")
+                 for e in args.epi.split(",") for f in args.pf2.split(",") for z in args.swz.split(",")
+                 for k in args.splitk.split(",") for t in args.tiles.split(",")]
         outs = {}
         times = {q: [] for q in paths}
         fn = lambda: ops.conv2d(x, p, res=res_t, act=ops.SILU)  # noqa: E731
@@ -68,6 +70,7 @@ def main():
             ops.set_conv_option(2, q[2])
             ops.set_conv_option(3, q[3])
             ops.SPLITK_ALLOWED = bool(q[4])
+            ops.set_conv_option(4, q[5])
             outs[q] = fn()
         for _ in range(3):
             for q in paths:
@@ -76,11 +79,12 @@ def main():
                 ops.set_conv_option(2, q[2])
                 ops.set_conv_option(3, q[3])
                 ops.SPLITK_ALLOWED = bool(q[4])
+                ops.set_conv_option(4, q[5])
                 times[q].append(bench(fn, args.reps))
         flops = 2.0 * B * (H // stride) * (W // stride) * cout * cin * k * k
         r = dict(name=name)
         for q in paths:
-            r["tf_" + "".join(f"{k}{v}" for k, v in zip("pefzk", q))] = round(flops / min(times[q]) / 1e12, 1)
+            r["tf_" + "".join(f"{k}{v}" for k, v in zip("pefzkt", q))] = round(flops / min(times[q]) / 1e12, 1)
         r["identical"] = all(torch.equal(outs[paths[0]], outs[q]) for q in paths if q[4] == 0)
         r["max_diff_splitk"] = max([(outs[paths[0]].float() - outs[q].float()).abs().max().item()
                                     for q in paths if q[4] == 1] or [0.0])
@@ -91,6 +95,7 @@ def main():
     ops.set_conv_option(2, 0)
     ops.set_conv_option(3, 1)
     ops.SPLITK_ALLOWED = False
+    ops.set_conv_option(4, -1)
 
 
 if __name__ == "__main__":
