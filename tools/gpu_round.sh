@@ -1,0 +1,19 @@
+# One GPU call: gpu tests, smoke, bench line, rocprofv3 kernel stats of the bench.
+# usage (repo root on the box): bash tools/gpu_round.sh TAG [tests|notests]
+set -e
+TAG=${1:-run}
+R=$PWD
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+if [ "${2:-tests}" = "tests" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+  echo "tests ok"
+  timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+  echo "smoke ok"
+fi
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err
+cat $O/bench.json
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_prof.json 2> $O/bench_prof.err
+echo "prof ok"
