@@ -72,9 +72,14 @@ typedef struct rdeic_conv_desc {
 } rdeic_conv_desc;
 
 int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
-/* rdeic_conv2d with an explicit tile for the big-tile path (0 256x256/16 waves, 1 256x128/8,
- * 2 128x256/8, 3 128x128/4, 4 64x128/4, 6 256x128/16, 7 128x256/16, 8 128x128/8, 9 128x128/16,
- * 10 64x128/8; -1 heuristic). All tiles give bit-identical results, so a caller may autotune. */
+/* rdeic_conv2d with an explicit tile. Register-staged tiles (any bf16 conv without a GN
+ * prologue): 0 256x256/16 waves, 1 256x128/8, 2 128x256/8, 3 128x128/4, 4 64x128/4,
+ * 6 256x128/16, 7 128x256/16, 8 128x128/8, 9 128x128/16, 10 64x128/8. LDS-DMA tiles (bf16, both
+ * concat segments multiples of 64 channels; other shapes fall back to the register path):
+ * 20 256x256/8, 21 256x128/8, 22 128x256/8, 23-24 128x128/4, 25 128x128/8, 26 64x128/4,
+ * 27 128x128/8, 28 256x128/8, 29 128x256/8, 30 64x128/4, 31 128x64/4, 32 256x256/16,
+ * 33 256x128/16, 34 128x128/16 (ring depths in conv_gemm.hip). -1 = heuristic. All tiles give
+ * bit-identical results (same k order, same MFMA), so a caller may autotune. */
 int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream);
 /* Split-K variant for small-M / large-K layers (the UNet's 8x8 and 16x16 levels): `splits`
  * k-ranges accumulate into the caller's fp32 workspace (>= splits * n*ho*wo * cout floats), then a
@@ -92,7 +97,8 @@ int rdeic_set_conv_path(int32_t path);
  * key 2: two-deep register prefetch in the register-staged conv path (0 default, 1 on);
  * key 3: XOR-swizzled 128-byte LDS rows on the <= 8-wave conv tiles (1 default) / padded rows (0);
  * key 4: force the big-tile candidate (0 256x256, 1 256x128, 2 128x256, 3 128x128, 4 64x128,
- *        5 128x64; -1 = automatic choice, default) — tuning only.
+ *        5 128x64; -1 = automatic choice, default) — tuning only;
+ * key 5: LDS-DMA conv kernel for 64-channel-aligned layers on (1, default) / off (0).
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way. */
 int rdeic_set_conv_option(int32_t key, int32_t value);
 

@@ -167,7 +167,8 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
         if tile is None:
             # scratch with the output's exact strides (out may be a channel slice of a wider buffer)
             scratch = torch.empty_strided(out.size(), out.stride(), dtype=out.dtype, device=out.device)
-            tile = _autotune_tile(d, scratch)
+            dma = x.dtype == torch.bfloat16 and c0 % 64 == 0 and c1 % 64 == 0
+            tile = _autotune_tile(d, scratch, DMA_TILE_CANDIDATES if dma else TILE_CANDIDATES)
             _TILE_CACHE[key] = tile
 
     def launch():
@@ -195,19 +196,22 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
 
 # Tile autotuning for the big-tile conv path: every candidate tile produces bit-identical results
 # (same k order, same MFMA), so the fastest one is picked per distinct layer shape on first use
-# (a few timed launches during warmup) and cached for the process.
+# (a few timed launches during warmup) and cached for the process. Layers whose channel
+# segments are multiples of 64 run on the LDS-DMA kernel (tile ids 20..34, rdeic_hip.h);
+# the others on the register-staged tiles.
 AUTOTUNE = True
 TILE_CANDIDATES = (0, 1, 3, 4, 6, 8, 10)
+DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31)
 _TILE_CACHE: dict = {}
 
 
-def _autotune_tile(d0, scratch: torch.Tensor) -> int:
+def _autotune_tile(d0, scratch: torch.Tensor, candidates=None) -> int:
     """Time each candidate writing into `scratch` (the real output may alias the residual)."""
     d = ConvDesc.from_buffer_copy(d0)
     d.out = scratch.data_ptr()
     s = stream_ptr()
     best, best_t = -1, float("inf")
-    for t in TILE_CANDIDATES:
+    for t in (TILE_CANDIDATES if candidates is None else candidates):
         call("rdeic_conv2d_tile", C.byref(d), t, s)  # warm (first launch of a kernel variant)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
