@@ -14,7 +14,7 @@ CXXFLAGS := -O3 -fPIC -std=c++17 -Wall -pthread
 
 all: $(LIB) oracle
 
-$(BUILD)/%.hip.o: rdeic_amd/csrc/%.hip rdeic_amd/csrc/common.h include/rdeic_hip.h
+$(BUILD)/%.hip.o: rdeic_amd/csrc/%.hip rdeic_amd/csrc/common.h rdeic_amd/csrc/prof.h include/rdeic_hip.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

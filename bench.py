@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--prof-every", type=int, default=8,
+                    help="time a hashed 1-in-N sample of the launches of each kind (roofline)")
+    ap.add_argument("--rate-gain", type=float, default=None,
+                    help="synthetic bpp knob (rdeic_amd/weights.py); default: the ~0.08 bpp gain of config 2")
     return ap.parse_args()
 
 
@@ -55,7 +59,9 @@ def main():
     torch.cuda.set_device(dev)
     B, S = args.batch, args.size
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    model = RDEIC(compute_dtype=dtype, device=dev).init_synthetic()
+    from rdeic_amd import weights as W
+    rate_gain = W.RATE_GAIN_BPP008 if args.rate_gain is None else args.rate_gain
+    model = RDEIC(compute_dtype=dtype, device=dev).init_synthetic(rate_gain=rate_gain)
     model.preprocess_model.update(force=True)
 
     g0 = rank * B  # global image indices of this rank's shard (weak scaling: B per GPU)
@@ -76,7 +82,9 @@ def main():
     for _ in range(args.warmup):
         step()
     if not args.no_roofline:
-        ops.PROFILE = []
+        # native launch profiler: the launchers record HIP events on their own stream for one launch
+        # in --prof-every of each kind (an event pair is two queue markers, i.e. GPU time)
+        ops.prof_start(2048 * max(1, args.steps) + 1024, args.prof_every)
     parallel.barrier(dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -85,7 +93,10 @@ def main():
     parallel.barrier(dev)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    prof, ops.PROFILE = ops.PROFILE, None
+    prof = None
+    if not args.no_roofline:
+        ops.prof_stop()
+        prof = ops.prof_read()
     elapsed = parallel.max_over_ranks(elapsed, dev)
     total_images = B * world * args.steps
     value = total_images / elapsed
@@ -93,21 +104,37 @@ def main():
         return
 
     roof = None
-    if prof:
-        n, flops, ms = ops.conv_profile_summary(prof)
+    if prof and "conv" in prof:
+        n, flops, ms = prof["conv"]
         achieved = flops / (ms * 1e-3) / 1e12
         peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_FP32_TFLOPS
         roof = {"bound": "mfma", "kernel": "conv_kernel (implicit-GEMM conv/linear, rdeic_conv2d)",
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": None, "launches_per_step": n // max(1, args.steps),
+                "traffic": None, "timed_launches": n, "sampled_one_in": args.prof_every,
                 "avg_launch_us": round(ms * 1e3 / max(1, n), 2),
-                "kernel_share_of_step": round(ms * 1e-3 / (elapsed / args.steps) / args.steps, 4)}
+                "kernel_share_of_step": round(ms * args.prof_every * 1e-3 / elapsed, 4)}
+        # secondary kernels the north star names: attention on MFMA, GroupNorm on HBM
+        sec = {}
+        for kind, (cnt, work, kms) in prof.items():
+            if kind == "conv" or kms <= 0:
+                continue
+            if kind.startswith("attention"):
+                a = work / (kms * 1e-3) / 1e12
+                sec[kind] = {"bound": "mfma", "achieved": round(a, 2), "peak": peak, "unit": "TFLOP/s",
+                             "frac": round(a / peak, 4), "timed_launches": cnt,
+                             "ms_per_step": round(kms * args.prof_every / args.steps, 3)}
+            else:
+                a = work / (kms * 1e-3) / 1e9
+                sec[kind] = {"bound": "hbm", "achieved": round(a, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(a / PEAK_HBM_GBS, 4), "timed_launches": cnt,
+                             "ms_per_step": round(kms * args.prof_every / args.steps, 3)}
+        roof["secondary"] = sec
     mrows = metrics.cpu().numpy()
     cpu = None
     if not args.no_cpu_baseline:
         try:
             from oracle.bench_cpu import run_cpu_baseline
-            cpu = run_cpu_baseline(size=S, steps=args.ddim_steps)
+            cpu = run_cpu_baseline(size=S, steps=args.ddim_steps, rate_gain=rate_gain)
         except Exception as e:  # the baseline is reported, never the target
             cpu = {"value": None, "error": f"{type(e).__name__}: {e}"}
     line = {
@@ -117,7 +144,7 @@ def main():
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded images, random-init weights)",
         "config": {"workload": f"config 2: batch {B}/GPU {S}x{S}, {args.ddim_steps}-step relay DDIM, "
                                f"encode+entropy-code+decode+VAE-decode", "global_batch": B * world,
-                   "image_size": S, "ddim_steps": args.ddim_steps, "parallelism": f"dp{world}",
+                   "image_size": S, "ddim_steps": args.ddim_steps, "parallelism": f"dp{world}", "rate_gain": rate_gain,
                    "mean_bpp": round(float(mrows[:, 0].mean()), 4),
                    "mean_psnr_db": round(float(mrows[:, 2].mean()), 2)},
         "roofline": roof,

@@ -233,6 +233,23 @@ int rdeic_ac_decode(const uint8_t* data, size_t len, size_t n, const int16_t* cd
 /* The uniform hyper-latent CDF of utils/ckbd.py:117-128 after torchac's int conversion. */
 int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row);
 
+/* --------------------------------------------------------- launch profiler
+ * The conv / attention / GroupNorm launchers bracket their kernels with HIP events on the
+ * launch stream while profiling is on (a preallocated ring of `capacity` event pairs, reused;
+ * launches beyond it are not recorded). Every event pair is a pair of queue markers that costs
+ * GPU time, so only a 1-in-`every` sample of each kind's launches is timed (hashed on the
+ * per-kind launch counter, so it does not alias with the per-step launch sequence). rdeic_prof_read sums, for one kind, the sampled launches, the
+ * algorithmic work (FLOPs for conv / attention, bytes for GroupNorm) and the event-timed ms
+ * (it synchronizes on the recorded events). rdeic_prof_stop returns the slots used. */
+#define RDEIC_PROF_CONV 0        /* rdeic_conv2d / _tile / _splitk (incl. batched GEMMs): 2*M*N*K FLOPs */
+#define RDEIC_PROF_ATTN 1        /* rdeic_attention, head dim >= 64: 4*B*H*Lq*Lk*dh FLOPs */
+#define RDEIC_PROF_ATTN_SMALL 2  /* rdeic_attention, head dim < 64 */
+#define RDEIC_PROF_GN_STATS 3    /* rdeic_groupnorm_stats: bytes read */
+#define RDEIC_PROF_GN_APPLY 4    /* rdeic_groupnorm_apply: bytes read + written */
+int rdeic_prof_start(int32_t capacity, int32_t every);
+int rdeic_prof_stop(void);
+int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms);
+
 #ifdef __cplusplus
 }
 #endif

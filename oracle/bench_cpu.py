@@ -13,14 +13,15 @@ import torch
 from . import model_ref as M
 
 
-def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads: int = None):
+def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads: int = None,
+                     rate_gain: float = 1.0):
     from rdeic_amd.synthetic import sampler_noise, synth_context, synth_image  # test-input generators
     if threads is None:
         threads = min(16, os.cpu_count() or 1)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
-        sd = M.synthetic_state_dict()
+        sd = M.synthetic_state_dict(rate_gain=rate_gain)
         tables = M.Tables()
         ctx = synth_context()
         imgs = [synth_image(size, size, 231 + i) for i in range(n_images)]

@@ -58,6 +58,9 @@ PROTOTYPES = {
     "rdeic_conv2d": (C.c_int, [C.POINTER(ConvDesc), _p]),
     "rdeic_conv2d_splitk": (C.c_int, [C.POINTER(ConvDesc), _i32, _p, C.c_size_t, _p]),
     "rdeic_conv2d_tile": (C.c_int, [C.POINTER(ConvDesc), _i32, _p]),
+    "rdeic_prof_start": (C.c_int, [_i32, _i32]),
+    "rdeic_prof_stop": (C.c_int, []),
+    "rdeic_prof_read": (C.c_int, [_i32, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rdeic_groupnorm_ws_floats": (_sz, [_i32, _i32, _i32]),
     "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p,
                                         _i32, _p]),
@@ -136,6 +139,15 @@ def check(name: str, rc: int) -> None:
         raise RdeicError(name, rc)
 
 
-def call(name: str, *args) -> None:
-    rc = getattr(load(), name)(*args)
+# When set to a list, every call() is also appended as (name, fn, args, tag) — rdeic_amd/plan.py
+# records a fixed-shape region's launch sequence this way and replays it without the Python layer
+# logic. `tag` = (kind, work, meta) marks launches bench.py times with events ("conv", FLOPs, ...).
+RECORDER = None
+
+
+def call(name: str, *args, tag=None) -> None:
+    fn = getattr(load(), name)
+    if RECORDER is not None:
+        RECORDER.append((name, fn, args, tag))
+    rc = fn(*args)
     check(name, rc)

@@ -15,6 +15,7 @@
 // (batched GEMM via rdeic_conv2d + rdeic_softmax_rows + GEMM), see rdeic_amd/ops.py.
 #include "common.h"
 #include "../../include/rdeic_hip.h"
+#include "prof.h"
 
 int rdeic_g_attn64 = 1;  // rdeic_set_conv_option(1, v): transposed dh=64 kernel on/off
 
@@ -459,6 +460,7 @@ extern "C" int rdeic_attention(const void* q, int32_t ldq, const void* k, int32_
   if (ldq % epc || ldk % epc || ldv % epc || ((uintptr_t)k) % 16 || ((uintptr_t)v) % 16 || ((uintptr_t)q) % 16)
     return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(s, dh >= 64 ? RDEIC_PROF_ATTN : RDEIC_PROF_ATTN_SMALL, 4.0 * batch * heads * (double)lq * lk * dh);
   if (dtype == 1) return launch_attn<bf16>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
   return launch_attn<float>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
 }

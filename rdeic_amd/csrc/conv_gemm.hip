@@ -20,6 +20,7 @@
 // Replaces: every nn.Conv2d / nn.Linear on the RDEIC hot path (see include/rdeic_hip.h).
 #include "common.h"
 #include "../../include/rdeic_hip.h"
+#include "prof.h"
 
 namespace {
 
@@ -1067,7 +1068,7 @@ int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec) {
 }
 }  // namespace
 
-extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
+static int conv2d_impl(const rdeic_conv_desc* d, void* stream) {
   ConvArgs a;
   bool vec = false;
   const int rc = make_args(d, a, vec);
@@ -1100,7 +1101,7 @@ extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
 // Explicit tile choice for the big-tile path (autotuning by the caller; every tile gives
 // bit-identical results). tile -1 = the built-in heuristic. Shapes outside the big-tile path
 // (GN prologue, cout <= 32, fp32, unaligned) ignore it and run exactly as rdeic_conv2d.
-extern "C" int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream) {
+static int conv2d_tile_impl(const rdeic_conv_desc* d, int32_t tile, void* stream) {
   ConvArgs a;
   bool vec = false;
   const int rc = make_args(d, a, vec);
@@ -1113,7 +1114,7 @@ extern "C" int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* s
     }
     return launch_plain_auto(a, (hipStream_t)stream, tile);
   }
-  return rdeic_conv2d(d, stream);
+  return conv2d_impl(d, stream);
 }
 
 // Split-K variant (small-M, large-K layers): `splits` k-ranges computed into a caller-provided
@@ -1121,8 +1122,8 @@ extern "C" int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* s
 // the bias / emb / activation / residual epilogue. bf16, 16-byte gathers, no GN prologue,
 // out_mode 0, batch 1, cout % 8 == 0. The k-order differs from rdeic_conv2d (not bit-identical
 // to it), so callers that need batch invariance must not use it.
-extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats,
-                                   void* stream) {
+static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats,
+                              void* stream) {
   ConvArgs a;
   bool vec = false;
   const int rc = make_args(d, a, vec);
@@ -1152,6 +1153,29 @@ extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, flo
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, a,
                      (const float*)ws);
   return launch_status();
+}
+
+// algorithmic FLOPs of one launch (2 per MAC), for the launch profiler
+static double conv_flops(const rdeic_conv_desc* d) {
+  if (!d) return 0.0;
+  const double b = d->batch > 1 ? d->batch : 1;
+  return 2.0 * b * d->n * d->ho * d->wo * d->cout * (double)d->kh * d->kw * (d->c0 + d->c1);
+}
+
+extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
+  ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
+  return conv2d_impl(d, stream);
+}
+
+extern "C" int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream) {
+  ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
+  return conv2d_tile_impl(d, tile, stream);
+}
+
+extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats,
+                                   void* stream) {
+  ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
+  return conv2d_splitk_impl(d, splits, ws, ws_floats, stream);
 }
 
 extern "C" int rdeic_set_conv_path(int32_t path) {

@@ -15,6 +15,7 @@
 // and nn.LayerNorm (attention.py:265-267).
 #include "common.h"
 #include "../../include/rdeic_hip.h"
+#include "prof.h"
 
 namespace {
 
@@ -366,6 +367,7 @@ extern "C" int rdeic_groupnorm_stats(const void* x0, int32_t c0, int32_t ld0, co
       c % groups != 0 || c / groups > 512)
     return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(s, RDEIC_PROF_GN_STATS, (double)n * hw * c * (dtype == 1 ? 2 : 4));
   if (dtype == 1) return gn_stats<bf16>(x0, c0, ld0, x1, c1, ld1, n, hw, groups, eps, gamma, beta, ab, ws, s);
   return gn_stats<float>(x0, c0, ld0, x1, c1, ld1, n, hw, groups, eps, gamma, beta, ab, ws, s);
 }
@@ -375,6 +377,7 @@ extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32
                                      void* stream) {
   if (!x || !ab || !y || n <= 0 || hw <= 0 || c <= 0 || ab_c < c) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(s, RDEIC_PROF_GN_APPLY, 2.0 * n * hw * c * (dtype == 1 ? 2 : 4));
   long total = (long)n * hw * c;
   if (dtype == 1 && c % 8 == 0 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
       ((uintptr_t)y) % 16 == 0 && ((uintptr_t)ab) % 16 == 0) {

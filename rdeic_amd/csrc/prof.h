@@ -1,0 +1,15 @@
+// Native launch profiler: HIP events recorded by the launchers themselves, on the stream each
+// kernel runs on, into a preallocated ring of event pairs (no allocation, no Python per launch).
+// Enabled by rdeic_prof_start(); bench.py reads per-kind totals with rdeic_prof_read() after
+// its timed region. Kinds: see include/rdeic_hip.h (RDEIC_PROF_*).
+#pragma once
+#include <hip/hip_runtime.h>
+
+int rdeic_prof_begin(hipStream_t s, int kind);                        // slot, or -1 (off / full / not sampled)
+void rdeic_prof_end(int slot, hipStream_t s, int kind, double work);  // no-op for slot < 0
+
+struct ProfScope {
+  int slot; hipStream_t s; int kind; double work;
+  ProfScope(hipStream_t s_, int kind_, double work_) : slot(rdeic_prof_begin(s_, kind_)), s(s_), kind(kind_), work(work_) {}
+  ~ProfScope() { rdeic_prof_end(slot, s, kind, work); }
+};

@@ -1,0 +1,80 @@
+// Native launch profiler (see prof.h).
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+#include "prof.h"
+#include "../../include/rdeic_hip.h"
+
+namespace {
+struct Slot { hipEvent_t a = nullptr, b = nullptr; int kind = -1; double work = 0.0; };
+std::vector<Slot> g_slots;
+int g_used = 0;
+bool g_on = false;
+int g_every = 1;     // time one launch in g_every (per kind)
+long g_seen[8] = {};
+std::mutex g_mu;
+}  // namespace
+
+int rdeic_prof_begin(hipStream_t s, int kind) {
+  if (!g_on) return -1;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_on || g_used >= (int)g_slots.size()) return -1;
+  if (kind >= 0 && kind < 8 && g_every > 1) {
+    // hashed sample (splitmix64 finaliser of the per-kind launch counter): unbiased even when the
+    // per-step launch count is a multiple of g_every
+    unsigned long long z = (unsigned long long)(g_seen[kind]++) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    if (z % (unsigned long long)g_every != 0) return -1;
+  }
+  const int i = g_used++;
+  g_slots[i].kind = -1;
+  if (hipEventRecord(g_slots[i].a, s) != hipSuccess) return -1;
+  return i;
+}
+
+void rdeic_prof_end(int slot, hipStream_t s, int kind, double work) {
+  if (slot < 0) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (hipEventRecord(g_slots[slot].b, s) != hipSuccess) return;
+  g_slots[slot].kind = kind;
+  g_slots[slot].work = work;
+}
+
+extern "C" int rdeic_prof_start(int32_t capacity, int32_t every) {
+  if (capacity <= 0 || every <= 0) return RDEIC_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  while ((int)g_slots.size() < capacity) {
+    Slot sl;
+    if (hipEventCreate(&sl.a) != hipSuccess || hipEventCreate(&sl.b) != hipSuccess) return RDEIC_ELAUNCH;
+    g_slots.push_back(sl);
+  }
+  g_used = 0;
+  g_every = every;
+  for (long& c : g_seen) c = 0;
+  g_on = true;
+  return RDEIC_OK;
+}
+
+extern "C" int rdeic_prof_stop(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_on = false;
+  return g_used;
+}
+
+extern "C" int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms) {
+  if (!launches || !work || !ms) return RDEIC_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  *launches = 0; *work = 0.0; *ms = 0.0;
+  for (int i = 0; i < g_used; ++i) {
+    const Slot& sl = g_slots[i];
+    if (sl.kind != kind) continue;
+    if (hipEventSynchronize(sl.b) != hipSuccess) return RDEIC_ELAUNCH;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, sl.a, sl.b) != hipSuccess) return RDEIC_ELAUNCH;
+    *launches += 1; *work += sl.work; *ms += t;
+  }
+  return RDEIC_OK;
+}

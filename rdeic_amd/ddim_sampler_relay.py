@@ -55,8 +55,9 @@ class DDIMSampler:
 
     @torch.no_grad()
     def sample_nhwc(self, S: int, x_T: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor,
-                    eta: float = 0.0) -> torch.Tensor:
-        """Internal path: x_T fp32 NHWC, guide_hint NHWC (compute dtype). Returns samples fp32 NHWC."""
+                    eta: float = 0.0, ts_tensors=None) -> torch.Tensor:
+        """Internal path: x_T fp32 NHWC, guide_hint NHWC (compute dtype). Returns samples fp32 NHWC.
+        ts_tensors: optional {timestep: int64 [B] device tensor} prepared outside a recorded plan."""
         self.make_schedule(S, ddim_eta=eta)
         if eta != 0.0:
             raise NotImplementedError("relay decoding uses eta = 0 (inference.py:78)")
@@ -66,7 +67,8 @@ class DDIMSampler:
         total = len(ts_all)
         for i, step in enumerate(ts_all):
             index = total - i - 1
-            ts = torch.full((B,), int(step), dtype=torch.long, device=x.device)
+            ts = (ts_tensors[int(step)] if ts_tensors is not None else
+                  torch.full((B,), int(step), dtype=torch.long, device=x.device))
             e = self.model.eps_nhwc(x, ts, guide_hint, context)
             c_sq1m, c_sqa, c_sqap, c_dir, _ = self._step_scalars(index)
             xp = torch.empty_like(x)

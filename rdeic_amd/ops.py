@@ -171,26 +171,14 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
             tile = _autotune_tile(d, scratch, DMA_TILE_CANDIDATES if dma else TILE_CANDIDATES)
             _TILE_CACHE[key] = tile
 
-    def launch():
-        if splits > 1:
-            ws = _splitk_workspace(splits * n * ho * wo * p.cout, x.device)
-            call("rdeic_conv2d_splitk", C.byref(d), splits, ws.data_ptr(), ws.numel(), stream_ptr())
-        elif tile >= 0:
-            call("rdeic_conv2d_tile", C.byref(d), tile, stream_ptr())
-        else:
-            call("rdeic_conv2d", C.byref(d), stream_ptr())
-
-    prof = PROFILE
-    if prof is not None:
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        launch()
-        ev1.record()
-        prof.append((flops, ev0, ev1, x.dtype,
-                     (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), int(pixel_shuffle))))
+    tag = ("conv", flops, (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), int(pixel_shuffle)))
+    if splits > 1:
+        ws = _splitk_workspace(splits * n * ho * wo * p.cout, x.device)
+        _launch(tag, "rdeic_conv2d_splitk", C.byref(d), splits, ws.data_ptr(), ws.numel(), stream_ptr())
+    elif tile >= 0:
+        _launch(tag, "rdeic_conv2d_tile", C.byref(d), tile, stream_ptr())
     else:
-        launch()
+        _launch(tag, "rdeic_conv2d", C.byref(d), stream_ptr())
     return out
 
 
@@ -207,6 +195,8 @@ _TILE_CACHE: dict = {}
 
 def _autotune_tile(d0, scratch: torch.Tensor, candidates=None) -> int:
     """Time each candidate writing into `scratch` (the real output may alias the residual)."""
+    if _lib.RECORDER is not None:  # never record tuning launches: keep the heuristic choice
+        return -1
     d = ConvDesc.from_buffer_copy(d0)
     d.out = scratch.data_ptr()
     s = stream_ptr()
@@ -268,7 +258,63 @@ def _splitk_workspace(n: int, device) -> torch.Tensor:
 
 # When set to a list, every rdeic_conv2d launch appends (algorithmic FLOPs, start event, end
 # event, dtype) — bench.py uses it to time the dominant kernel live over its timed region.
+# The secondary kernels (attention: FLOPs; GroupNorm statistics / apply: algorithmic bytes) go to
+# PROFILE_OTHER[kind] as (work, start event, end event) while PROFILE is set.
 PROFILE = None
+PROFILE_OTHER: dict = {}
+
+
+def _launch(tag, name: str, *args):
+    """call(name, *args); when profiling, bracket it with events on the current stream and file it
+    under tag = (kind, work, meta): "conv" -> PROFILE, anything else -> PROFILE_OTHER[kind]."""
+    if PROFILE is None:
+        return call(name, *args, tag=tag)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    call(name, *args, tag=tag)
+    ev1.record()
+    record_profile(tag, ev0, ev1)
+
+
+def record_profile(tag, ev0, ev1):
+    kind, work, meta = tag
+    if kind == "conv":
+        PROFILE.append((work, ev0, ev1, None, meta))
+    else:
+        PROFILE_OTHER.setdefault(kind, []).append((work, ev0, ev1))
+
+
+PROF_KINDS = {"conv": 0, "attention": 1, "attention_dh16": 2, "gn_stats": 3, "gn_apply": 4}
+
+
+def prof_start(capacity: int = 65536, every: int = 1) -> None:
+    """Native launch profiler (rdeic_prof_*): the launchers record HIP events on their stream,
+    for one launch in `every` of each kind."""
+    call("rdeic_prof_start", capacity, every)
+
+
+def prof_stop() -> int:
+    return int(_lib.load().rdeic_prof_stop())
+
+
+def prof_read() -> dict:
+    """{kind: (launches, algorithmic work, event-timed ms)} recorded since prof_start (synchronizes)."""
+    out = {}
+    for kind, code in PROF_KINDS.items():
+        n, w, ms = C.c_int64(), C.c_double(), C.c_double()
+        call("rdeic_prof_read", code, C.byref(n), C.byref(w), C.byref(ms))
+        if n.value:
+            out[kind] = (n.value, w.value, ms.value)
+    return out
+
+
+def other_profile_summary():
+    """{kind: (launches, total work, total ms)} of the secondary kernels (after sync)."""
+    out = {}
+    for kind, recs in PROFILE_OTHER.items():
+        out[kind] = (len(recs), sum(r[0] for r in recs), sum(r[1].elapsed_time(r[2]) for r in recs))
+    return out
 
 
 def conv_profile_summary(records):
@@ -356,16 +402,7 @@ def gemm_batched(a: torch.Tensor, b_nk: torch.Tensor, out: torch.Tensor, *, batc
     d.out_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
     d.batch = batch
     d.in_bs, d.w_bs, d.out_bs = a_bs, b_bs, out_bs
-    prof = PROFILE
-    if prof is not None:
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        call("rdeic_conv2d", C.byref(d), stream_ptr())
-        ev1.record()
-        prof.append((2.0 * batch * m * n * k, ev0, ev1, a.dtype, ("bgemm", batch, m, n, k)))
-    else:
-        call("rdeic_conv2d", C.byref(d), stream_ptr())
+    _launch(("conv", 2.0 * batch * m * n * k, ("bgemm", batch, m, n, k)), "rdeic_conv2d", C.byref(d), stream_ptr())
     return out
 
 
@@ -378,8 +415,9 @@ def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, grou
     c = c0 + c1
     ws = torch.empty(int(_lib.load().rdeic_groupnorm_ws_floats(n, h * w, c)), dtype=torch.float32, device=x.device)
     ab = torch.empty((n, c, 2), dtype=torch.float32, device=x.device)
-    call("rdeic_groupnorm_stats", x.data_ptr(), c0, ld0, _ptr(x2), c1, ld1, n, h * w, groups, float(eps),
-         gamma.data_ptr(), beta.data_ptr(), ab.data_ptr(), ws.data_ptr(), dt_code(x), stream_ptr())
+    _launch(("gn_stats", float(n * h * w * c * x.element_size()), None),
+            "rdeic_groupnorm_stats", x.data_ptr(), c0, ld0, _ptr(x2), c1, ld1, n, h * w, groups,
+            float(eps), gamma.data_ptr(), beta.data_ptr(), ab.data_ptr(), ws.data_ptr(), dt_code(x), stream_ptr())
     return ab
 
 
@@ -391,8 +429,9 @@ def group_norm_apply(x: torch.Tensor, ab: torch.Tensor, silu: bool, out: Optiona
         out = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)
     if ab.shape[1] < c or ab.stride(2) != 1 or ab.stride(1) != 2:
         raise ValueError("group-norm affine must be [n, >=c, 2] with packed (a, b) pairs")
-    call("rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(), ab.stride(0) // 2, int(silu),
-         float(out_mul), out.data_ptr(), pix_ld(out), dt_code(x), stream_ptr())
+    _launch(("gn_apply", float(2 * n * h * w * c * x.element_size()), None),
+            "rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(),
+            ab.stride(0) // 2, int(silu), float(out_mul), out.data_ptr(), pix_ld(out), dt_code(x), stream_ptr())
     return out
 
 
@@ -410,9 +449,10 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
               lq: int, lk: int, dh: int, scale: float, kv_bcast: bool = False) -> torch.Tensor:
     """Flash attention over [batch*lq, heads*dh]-layout projections (row strides from the tensors).
     kv_bcast: K/V hold one batch shared by every query batch."""
-    call("rdeic_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
-         out.data_ptr(), out.stride(0), batch, heads, lq, lk, dh, float(scale), int(kv_bcast), dt_code(q),
-         stream_ptr())
+    _launch(("attention" if dh >= 64 else "attention_dh%d" % dh, 4.0 * batch * heads * lq * lk * dh, None),
+            "rdeic_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(),
+            v.stride(0), out.data_ptr(), out.stride(0), batch, heads, lq, lk, dh, float(scale),
+            int(kv_bcast), dt_code(q), stream_ptr())
     return out
 
 

@@ -45,10 +45,10 @@ class ParamStore:
         self.declare(prefix + ".bias", (c,))
 
     # ------------------------------------------------------------ materialisation
-    def init_synthetic(self, global_seed: int = W.GLOBAL_SEED):
+    def init_synthetic(self, global_seed: int = W.GLOBAL_SEED, rate_gain: float = 1.0):
         """Counter-based synthetic weights generated on device (bit-identical to the oracle's)."""
         for name, shape in self.shapes.items():
-            scale, offset = W.init_spec(name, shape)
+            scale, offset = W.init_spec(name, shape, rate_gain)
             t = torch.empty(shape, dtype=torch.float32, device=self.device)
             ops.fill_uniform(t, W.param_seed(name, global_seed), scale, offset)
             self.t[name] = t

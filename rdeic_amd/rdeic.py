@@ -65,15 +65,21 @@ class RDEIC:
         self.device = torch.device(device)
         for k, v in sched.items():
             setattr(self, k, v.to(self.device))
+        from .plan import PlanCache
+        self.use_plans = True
+        self._plans = PlanCache()
+        self._consts = {}
 
     # ------------------------------------------------------------------ weights
     @property
     def compute_dtype(self):
         return self.store.compute_dtype
 
-    def init_synthetic(self, seed: Optional[int] = None):
+    def init_synthetic(self, seed: Optional[int] = None, rate_gain: float = 1.0):
+        """Synthetic weights (rdeic_amd/weights.py); rate_gain is the bpp knob (weights.RATE_LAYERS)."""
         from . import weights as W
-        self.store.init_synthetic(W.GLOBAL_SEED if seed is None else seed)
+        self.store.init_synthetic(W.GLOBAL_SEED if seed is None else seed, rate_gain)
+        self._plans.clear()  # recorded plans point at the previous packed weights
         self.preprocess_model._en = None
         return self
 
@@ -81,6 +87,7 @@ class RDEIC:
         """Load reference-named weights (e.g. a RDEIC checkpoint's state_dict). Non-parameter buffers of the
         reference (schedules, entropy tables, scale_list, cond_stage_model) are ignored."""
         self.store.load_state_dict({k: v for k, v in sd.items() if k in self.store.shapes}, strict=strict)
+        self._plans.clear()
         self.preprocess_model._en = None
         return self
 
@@ -114,12 +121,12 @@ class RDEIC:
     def eps_nhwc(self, x: torch.Tensor, t: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor):
         return self.control_model.forward(x, guide_hint, t, context.to(self.device))
 
-    def decode_nhwc(self, z: torch.Tensor, out_f32: bool = True) -> torch.Tensor:
+    def decode_nhwc(self, z: torch.Tensor, out_f32: bool = True, consts=None) -> torch.Tensor:
         """z: fp32 NHWC latent sample -> decoder output NHWC [B,8h,8w,3] (1/scale_factor fused)."""
         B = z.shape[0]
         zs = torch.empty_like(z)
-        inv = torch.full((B,), 1.0 / self.scale_factor, dtype=torch.float32, device=z.device)
-        zero = torch.zeros((B,), dtype=torch.float32, device=z.device)
+        consts = consts or self._region_consts(B, 0, z.device)
+        inv, zero = consts["inv_scale"], consts["zero"]
         ops.call("rdeic_axpby", z.contiguous().data_ptr(), z.contiguous().data_ptr(), B, z[0].numel(), inv.data_ptr(),
                  zero.data_ptr(), zs.data_ptr(), ops.stream_ptr())
         zc = ops.cast(zs, self.compute_dtype)
@@ -199,6 +206,47 @@ class RDEIC:
         x = self.q_sample_nhwc(c_latent, t, noise)
         return DDIMSampler(self).sample_nhwc(steps, x, guide_hint, context)
 
+    def _region_consts(self, B: int, steps: int, device) -> dict:
+        """Per-(batch, steps) device constants of the relay + decode region, made outside any
+        recorded launch plan (a plan replays only librdeic_hip launches)."""
+        key = (B, steps, str(device))
+        c = self._consts.get(key)
+        if c is None:
+            from .ddim_sampler_relay import make_ddim_timesteps
+            t = torch.full((B,), self.used_timesteps - 1, dtype=torch.long, device=device)
+            c = {"qa": self.sqrt_alphas_cumprod[t].contiguous(), "qb": self.sqrt_one_minus_alphas_cumprod[t].contiguous(),
+                 "inv_scale": torch.full((B,), 1.0 / self.scale_factor, dtype=torch.float32, device=device),
+                 "zero": torch.zeros((B,), dtype=torch.float32, device=device), "ts": {}}
+            if steps:
+                for st in make_ddim_timesteps(steps, self.used_timesteps):
+                    c["ts"][int(st)] = torch.full((B,), int(st), dtype=torch.long, device=device)
+            self._consts[key] = c
+        return c
+
+    def _relay_decode_u8(self, c_latent, guide_hint, context, noise, steps: int):
+        """q_sample(c_latent, 299, noise) -> relay DDIM -> VAE decode -> uint8 NHWC (launches only)."""
+        from .ddim_sampler_relay import DDIMSampler
+        B = c_latent.shape[0]
+        c = self._region_consts(B, steps, c_latent.device)
+        x = torch.empty_like(c_latent)
+        ops.call("rdeic_axpby", c_latent.data_ptr(), noise.data_ptr(), B, c_latent[0].numel(), c["qa"].data_ptr(),
+                 c["qb"].data_ptr(), x.data_ptr(), ops.stream_ptr())
+        z = DDIMSampler(self).sample_nhwc(steps, x, guide_hint, context, ts_tensors=c["ts"])
+        return self.to_image_u8(self.decode_nhwc(z, out_f32=True, consts=c))
+
+    @torch.no_grad()
+    def relay_decode_u8(self, c_latent: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor,
+                        noise: torch.Tensor, steps: int) -> torch.Tensor:
+        """Relay denoise + VAE decode of a batch to uint8 [B,H,W,3]. With use_plans (default) the
+        fixed-shape launch sequence is recorded once per shape and replayed (rdeic_amd/plan.py);
+        the result is bit-identical to the eager path."""
+        ctx = context.to(device=self.device, dtype=self.compute_dtype).contiguous()
+        ins = [c_latent.contiguous(), guide_hint.contiguous(), ctx, noise.contiguous()]
+        if not self.use_plans:
+            return self._relay_decode_u8(*ins, steps)
+        key = ("relay_decode", steps) + tuple((tuple(t.shape), t.dtype) for t in ins)
+        return self._plans.run(key, lambda a, b, c, d: self._relay_decode_u8(a, b, c, d, steps), ins).clone()
+
     @torch.no_grad()
     def codec_images(self, img_u8: torch.Tensor, context: torch.Tensor, noise_nchw: torch.Tensor, steps: int = 2):
         """The full hot path on a batch: compress -> bytes -> decompress -> relay denoise -> VAE decode -> u8.
@@ -206,5 +254,4 @@ class RDEIC:
         bodies = self.compress_images(img_u8)
         c_lat, hint = self.decompress_bodies(bodies)
         noise = ops.nchw_to_nhwc(noise_nchw.float().to(self.device), torch.float32)
-        z = self.relay_sample_nhwc(c_lat, hint, context, noise, steps)
-        return self.to_image_u8(self.decode_nhwc(z, out_f32=True)), bodies
+        return self.relay_decode_u8(c_lat, hint, context, noise, steps), bodies

@@ -145,3 +145,30 @@ def test_codec_bf16_self_consistent(gpu, gold, model32):
     diff = (out16.float() - out32.float()).abs()
     print(f"bf16 vs fp32 reconstruction: mean |d| {diff.mean().item():.2f} / 255, max {diff.max().item():.0f}")
     assert diff.mean().item() < 8.0
+
+
+def test_low_rate_bitstream_vs_oracle(gpu, gold):
+    """The bench's ~0.08 bpp synthetic regime (weights.RATE_GAIN_BPP008): fp32 GPU files equal
+    the CPU oracle's (same weight spec, C rANS twin) and the bf16 path decodes its own streams."""
+    from oracle import model_ref as M
+    from rdeic_amd import weights as W
+    from rdeic_amd.rdeic import RDEIC
+    g = W.RATE_GAIN_BPP008
+    m32 = RDEIC(compute_dtype=torch.float32).init_synthetic(rate_gain=g)
+    imgs = torch.from_numpy(np.stack([gold["img0_in"], gold["img1_in"]])).cuda()
+    bodies = m32.compress_images(imgs)
+    sd = M.synthetic_state_dict(rate_gain=g)
+    tables = M.Tables()
+    with torch.no_grad():
+        for i in range(2):
+            x = torch.tensor(gold[f"img{i}_in"][None] / 255.0, dtype=torch.float32).permute(0, 3, 1, 2).contiguous()
+            body, _, _ = M.compress(sd, M.vae_encode_hc(sd, x * 2 - 1) * 0.18215, tables, coder="c")
+            assert bodies[i] == body, f"image {i}: {len(bodies[i])} vs oracle {len(body)} bytes"
+    print("low-rate bpp:", [8.0 * len(b) / (128 * 128) for b in bodies])
+    m16 = RDEIC(compute_dtype=torch.bfloat16).init_synthetic(rate_gain=g)
+    b16 = m16.compress_images(imgs)
+    c_b, h_b = m16.decompress_bodies(b16)
+    solo = m16.compress_images(imgs[:1])
+    assert solo[0] == b16[0]
+    c_s, _ = m16.decompress_bodies(b16[:1])
+    assert torch.equal(c_b[:1], c_s)
