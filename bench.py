@@ -30,6 +30,20 @@ PEAK_FP32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
+def conv_traffic():
+    """HBM bytes per conv launch, from the latest committed PMC run (tools/pmc_bench.sh ->
+    profiles/conv_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md §HBM). Counters cannot be read inside this process, so the figure is the
+    measured one with its source, or None when no PMC run has been committed."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "conv_traffic.json")) as f:
+            t = json.load(f)
+        return {"bytes_per_launch": t["bytes_per_launch"], "algorithmic_flops_per_launch": t.get("flops_per_launch"),
+                "source": t.get("source", "profiles/conv_traffic.json")}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -42,7 +56,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--prof-every", type=int, default=8,
-                    help="time a hashed 1-in-N sample of the launches of each kind (roofline)")
+                    help="roofline timing: every launch >= 50 GFLOP (64 MB for GroupNorm), and a hashed "
+                         "1-in-N sample of the smaller ones (weighted estimate)")
+    ap.add_argument("--coder-groups", type=int, default=None,
+                    help="image groups interleaved in the entropy-stage loops (default: the library's)")
+    ap.add_argument("--no-plans", action="store_true", help="eager launches (no launch-plan replay), A/B only")
     ap.add_argument("--rate-gain", type=float, default=None,
                     help="synthetic bpp knob (rdeic_amd/weights.py); default: the ~0.08 bpp gain of config 2")
     return ap.parse_args()
@@ -63,6 +81,10 @@ def main():
     rate_gain = W.RATE_GAIN_BPP008 if args.rate_gain is None else args.rate_gain
     model = RDEIC(compute_dtype=dtype, device=dev).init_synthetic(rate_gain=rate_gain)
     model.preprocess_model.update(force=True)
+    if args.coder_groups is not None:
+        model.preprocess_model.coder_groups = args.coder_groups
+    if args.no_plans:
+        model.use_plans = False
 
     g0 = rank * B  # global image indices of this rank's shard (weak scaling: B per GPU)
     imgs = torch.from_numpy(np.stack([synth_image(S, S, 231 + g0 + i) for i in range(B)])).to(dev)
@@ -108,11 +130,12 @@ def main():
         n, flops, ms = prof["conv"]
         achieved = flops / (ms * 1e-3) / 1e12
         peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_FP32_TFLOPS
-        roof = {"bound": "mfma", "kernel": "conv_kernel (implicit-GEMM conv/linear, rdeic_conv2d)",
+        roof = {"bound": "mfma", "kernel": "conv_dma_kernel / conv_kernel (implicit-GEMM conv + linear, rdeic_conv2d)",
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": None, "timed_launches": n, "sampled_one_in": args.prof_every,
-                "avg_launch_us": round(ms * 1e3 / max(1, n), 2),
-                "kernel_share_of_step": round(ms * args.prof_every * 1e-3 / elapsed, 4)}
+                "traffic": conv_traffic(), "launches_per_step": round(n / args.steps, 1),
+                "sampling": f"launches >= 50 GFLOP always timed, smaller ones 1 in {args.prof_every} (weighted)",
+                "avg_launch_us": round(ms * 1e3 / max(1, n), 2), "ms_per_step": round(ms / args.steps, 3),
+                "kernel_share_of_step": round(ms * 1e-3 / elapsed, 4)}
         # secondary kernels the north star names: attention on MFMA, GroupNorm on HBM
         sec = {}
         for kind, (cnt, work, kms) in prof.items():
@@ -121,13 +144,13 @@ def main():
             if kind.startswith("attention"):
                 a = work / (kms * 1e-3) / 1e12
                 sec[kind] = {"bound": "mfma", "achieved": round(a, 2), "peak": peak, "unit": "TFLOP/s",
-                             "frac": round(a / peak, 4), "timed_launches": cnt,
-                             "ms_per_step": round(kms * args.prof_every / args.steps, 3)}
+                             "frac": round(a / peak, 4), "launches_per_step": round(cnt / args.steps, 1),
+                             "ms_per_step": round(kms / args.steps, 3)}
             else:
                 a = work / (kms * 1e-3) / 1e9
                 sec[kind] = {"bound": "hbm", "achieved": round(a, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(a / PEAK_HBM_GBS, 4), "timed_launches": cnt,
-                             "ms_per_step": round(kms * args.prof_every / args.steps, 3)}
+                             "frac": round(a / PEAK_HBM_GBS, 4), "launches_per_step": round(cnt / args.steps, 1),
+                             "ms_per_step": round(kms / args.steps, 3)}
         roof["secondary"] = sec
     mrows = metrics.cpu().numpy()
     cpu = None

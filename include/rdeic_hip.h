@@ -237,8 +237,10 @@ int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row);
  * The conv / attention / GroupNorm launchers bracket their kernels with HIP events on the
  * launch stream while profiling is on (a preallocated ring of `capacity` event pairs, reused;
  * launches beyond it are not recorded). Every event pair is a pair of queue markers that costs
- * GPU time, so only a 1-in-`every` sample of each kind's launches is timed (hashed on the
- * per-kind launch counter, so it does not alias with the per-step launch sequence). rdeic_prof_read sums, for one kind, the sampled launches, the
+ * GPU time, so launches of at least 50 GFLOP (conv / attention) or 64 MB (GroupNorm) are always
+ * timed and the smaller ones in a 1-in-`every` sample (hashed on the per-kind launch counter, so
+ * it does not alias with the per-step launch sequence), each sampled launch weighted by `every`.
+ * rdeic_prof_read returns, for one kind, the weighted estimates of the launch count, the
  * algorithmic work (FLOPs for conv / attention, bytes for GroupNorm) and the event-timed ms
  * (it synchronizes on the recorded events). rdeic_prof_stop returns the slots used. */
 #define RDEIC_PROF_CONV 0        /* rdeic_conv2d / _tile / _splitk (incl. batched GEMMs): 2*M*N*K FLOPs */

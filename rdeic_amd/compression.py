@@ -18,6 +18,12 @@ Entropy stage (10 slices x {anchor, non-anchor}, compression.py:171-203 / 233-26
 The reference codes batch 1 per call (utils/ckbd.py:140 hard-codes batch 1 on decode); every
 kernel here is batch-invariant (fixed reduction order), so a batched call produces exactly the
 per-image streams and reconstructions of B single-image calls.
+
+Host/GPU overlap: the batch is split into `coder_groups` image groups whose stage sequences run
+interleaved (generators that yield at every host round trip), so while the host rANS-codes one
+group's stage the GPU runs the stages the other group has queued. The GPU part of compress and of
+decompress, with the host coder steps at their places in the sequence (plan.host_step), is
+recorded once per shape as a launch plan and replayed (rdeic_amd/plan.py).
 """
 from __future__ import annotations
 
@@ -28,6 +34,7 @@ import torch
 
 from . import coders, ops
 from .params import ParamStore
+from .plan import PlanCache, host_step
 
 LEAK = 0.01
 
@@ -75,6 +82,12 @@ class Compression:
         d.declare(f"{p}quantize.embedding.weight", (codebook_size, N))
         self.tables = None
         self._en = None
+        # image groups interleaved in the stage loops: measured on MI355X (B=16, 512^2) 2 groups cost
+        # more GPU time (twice the small stage launches) than the host overlap saves, so 1
+        self.coder_groups = 1
+        self.use_plans = True
+        self._plans = PlanCache()
+        self._io = {}              # per-call host state read by the recorded host steps
 
     def _declare_block(self, pre, kind, ci, co):
         d = self.store
@@ -98,6 +111,7 @@ class Compression:
         """GaussianConditional.update_scale_table(get_scale_table()) (compression.py:275-280)."""
         if self.tables is None or force or scale_table is not None:
             self.tables = coders.GaussianTables(scale_table)
+            self._plans.clear()  # recorded plans hold the previous device scale table
         return True
 
     # ------------------------------------------------------------------ nets
@@ -189,11 +203,12 @@ class Compression:
         anchor = torch.empty((B, hy, wy, cmax), dtype=dt, device=device)
         return yhat, ctx, anchor
 
-    def _run_stages(self, hyper, B, hy, wy, emit):
-        """Drive the 20 checkerboard stages. emit(i, phase, params, c, off, yhat_slice, anchor_buf)
-        produces the dequantised slice values (encode: from y; decode: from the bitstream)."""
-        dt, dev = hyper.dtype, hyper.device
-        yhat, ctxbuf, anchor_full = self._stage_common(hy, wy, B, dev, dt)
+    def _stage_gen(self, hyper, hy, wy, emit, bufs):
+        """Generator over the 20 checkerboard stages of one image group (hyper and bufs are that
+        group's batch slices). emit(i, phase, params, c, off, yhat_slice, anchor_buf) produces the
+        dequantised slice values (encode: from y; decode: from the bitstream). It may return a
+        generator, whose yields mark the host round trips other groups can overlap."""
+        yhat, ctxbuf, anchor_full = bufs
         off = 0
         for i, c in enumerate(self.slice_ch):
             s0 = self.slice_off[i]
@@ -204,21 +219,55 @@ class Compression:
             else:
                 self._channel_ctx(i, yhat[..., :s0], out=ctx[..., 2 * c:4 * c])
                 pa = self._ep("entropy_parameters_anchor", i, ctx[..., 2 * c:4 * c], hyper)
-            emit(i, 0, pa, c, off, yhat[..., s0:s0 + c], anchor)
+            r = emit(i, 0, pa, c, off, yhat[..., s0:s0 + c], anchor)
+            if r is not None:
+                yield from r
             off += c * hy * (wy // 2)
             ops.conv2d(anchor, self.store.conv(f"{self.p}local_context.{i}"), out=ctx[..., :2 * c])
             pn = self._ep("entropy_parameters_nonanchor", i, ctx[..., :(4 * c if i else 2 * c)], hyper)
-            emit(i, 1, pn, c, off, yhat[..., s0:s0 + c], None)
+            r = emit(i, 1, pn, c, off, yhat[..., s0:s0 + c], None)
+            if r is not None:
+                yield from r
             off += c * hy * (wy // 2)
-        return yhat
+
+    def _run_stages(self, hyper, B, hy, wy, emit):
+        """The 20 stages for the whole batch as one group."""
+        bufs = self._stage_common(hy, wy, B, hyper.device, hyper.dtype)
+        for _ in self._stage_gen(hyper, hy, wy, emit, bufs):
+            pass
+        return bufs[0]
+
+    def _groups(self, B: int) -> List[Tuple[int, int]]:
+        g = max(1, min(int(self.coder_groups), B))
+        cut = [B * k // g for k in range(g + 1)]
+        return [(cut[k], cut[k + 1]) for k in range(g)]
+
+    @staticmethod
+    def _interleave(gens) -> None:
+        """Round-robin over the groups' stage generators (one stream; host waits are per-event,
+        so a group's host step never waits for GPU work queued after it)."""
+        live = list(gens)
+        while live:
+            for g in list(live):
+                try:
+                    next(g)
+                except StopIteration:
+                    live.remove(g)
+
+    def _run_region(self, name, fn, inputs, before=None):
+        """fn(*inputs) eagerly, or recorded once per shape and replayed (launch plan)."""
+        if not self.use_plans:
+            if before is not None:
+                before()
+            return fn(*inputs)
+        key = (name, self.coder_groups) + tuple((tuple(t.shape), t.dtype) for t in inputs)
+        return self._plans.run(key, fn, inputs, before=before)
 
     # ------------------------------------------------------------------ compress / decompress
-    @torch.no_grad()
-    def compress(self, h: torch.Tensor) -> List[dict]:
-        """h: NHWC [B, H/8, W/8, 512] (compute dtype). Returns one reference-format dict per image:
-        {"strings": [[y_string], [z_string]], "shape": (zh, zw)} (compression.py:151-213)."""
-        self.update()
-        s = self.store
+    def _compress_gpu(self, h: torch.Tensor) -> torch.Tensor:
+        """compress() up to the bytes of the z indexes: nets, VQ, the 20 stages, and (host steps)
+        the rANS coding of each image group into self._io["y_strings"]. Returns the pinned host
+        copy of the VQ indexes [B, hz, wz], complete once the region has run."""
         B = h.shape[0]
         y = self._seq(self.g_a, h)
         z = self._seq(self.hyper_enc, y)
@@ -226,34 +275,127 @@ class Compression:
         hyper = self._seq(self.hyper_dec, z_q)
         _, hy, wy, _ = y.shape
         total = sum(self.stage_sizes(hy, wy))
-        sym = torch.empty((B, total), dtype=torch.int32, device=h.device)
-        idx = torch.empty((B, total), dtype=torch.int32, device=h.device)
         table = self.tables.device_scale_table(h.device)
         dtc = ops.dt_code(h)
+        bufs = self._stage_common(hy, wy, B, h.device, hyper.dtype)
+        zi_p = self._pinned("enc_zidx", z_idx.numel()).view(z_idx.shape)
+        host_step(lambda: zi_p.copy_(z_idx, non_blocking=True))
 
-        def emit(i, phase, params, c, off, yhat_slice, anchor):
-            s0 = self.slice_off[i]
-            ys = y[..., s0:s0 + c]
-            ops.call("rdeic_ckbd_encode", ys.data_ptr(), ops.pix_ld(ys), params.data_ptr(), ops.pix_ld(params), B, hy,
-                     wy, c, phase, table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), sym.data_ptr(),
-                     idx.data_ptr(), total, off, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
-                     None if anchor is None else anchor.data_ptr(), 0 if anchor is None else ops.pix_ld(anchor), dtc,
-                     ops.stream_ptr())
+        def group(gi: int, b0: int, b1: int):
+            nb = b1 - b0
+            yg = y[b0:b1]
+            sym = torch.empty((nb, total), dtype=torch.int32, device=h.device)
+            idx = torch.empty((nb, total), dtype=torch.int32, device=h.device)
+            sym_p = self._pinned(f"enc_sym{gi}", nb * total).view(nb, total)
+            idx_p = self._pinned(f"enc_idx{gi}", nb * total).view(nb, total)
+            done = torch.cuda.Event()
 
-        self._run_stages(hyper, B, hy, wy, emit)
-        sym_p = self._pinned("enc_sym", B * total).view(B, total)
-        idx_p = self._pinned("enc_idx", B * total).view(B, total)
-        sym_p.copy_(sym, non_blocking=True)
-        idx_p.copy_(idx, non_blocking=True)
-        zi = z_idx.cpu().numpy()  # synchronises the stream: the pinned copies above are complete
-        sym_h, idx_h = sym_p.numpy(), idx_p.numpy()
-        y_strings = coders.rans_encode_batch(sym_h, idx_h, self.tables)
-        hz, wz = z.shape[1], z.shape[2]
+            def emit(i, phase, params, c, off, yhat_slice, anchor):
+                s0 = self.slice_off[i]
+                ys = yg[..., s0:s0 + c]
+                ops.call("rdeic_ckbd_encode", ys.data_ptr(), ops.pix_ld(ys), params.data_ptr(), ops.pix_ld(params), nb,
+                         hy, wy, c, phase, table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), sym.data_ptr(),
+                         idx.data_ptr(), total, off, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
+                         None if anchor is None else anchor.data_ptr(), 0 if anchor is None else ops.pix_ld(anchor),
+                         dtc, ops.stream_ptr())
+
+            yield from self._stage_gen(hyper[b0:b1], hy, wy, emit, [t[b0:b1] for t in bufs])
+
+            def to_host():
+                sym_p.copy_(sym, non_blocking=True)
+                idx_p.copy_(idx, non_blocking=True)
+                done.record()
+
+            host_step(to_host)
+            yield  # the next group's stages are queued before this group is coded
+
+            def code():
+                done.synchronize()
+                self._io["y_strings"][b0:b1] = coders.rans_encode_batch(sym_p.numpy(), idx_p.numpy(), self.tables)
+
+            host_step(code)
+
+        self._interleave([group(gi, b0, b1) for gi, (b0, b1) in enumerate(self._groups(B))])
+        return zi_p
+
+    def compress_with(self, front, x: torch.Tensor) -> List[dict]:
+        """compress(front(x)), with front's launches (e.g. the VAE encoder; launch-only) inside the
+        same recorded region."""
+        self.update()
+        B = x.shape[0]
+        self._io = {"y_strings": [b""] * B}
+        try:
+            zi = self._run_region("compress", lambda t: self._compress_gpu(front(t)), [x]).numpy()
+            y_strings = self._io["y_strings"]
+        finally:
+            self._io = {}
+        hz, wz = zi.shape[1], zi.shape[2]
         out = []
         for b in range(B):
             z_str = coders.ac_encode_uniform(zi[b], self.codebook_size)
             out.append({"strings": [[y_strings[b]], [z_str]], "shape": (hz, wz)})
         return out
+
+    @torch.no_grad()
+    def compress(self, h: torch.Tensor) -> List[dict]:
+        """h: NHWC [B, H/8, W/8, 512] (compute dtype). Returns one reference-format dict per image:
+        {"strings": [[y_string], [z_string]], "shape": (zh, zw)} (compression.py:151-213)."""
+        return self.compress_with(lambda t: t, h)
+
+    def _decompress_gpu(self, z_idx: torch.Tensor):
+        """decompress() from the device VQ indexes on: codebook, hyper decoder, the 20 stages with
+        their rANS round trips (host steps, decoders in self._io["decs"]), g_s and the out conv."""
+        B, hz, wz = z_idx.shape
+        z_q = self.codebook_entry(z_idx, B, hz, wz)
+        hyper = self._seq(self.hyper_dec, z_q)
+        _, hy, wy, _ = hyper.shape
+        dev = hyper.device
+        table = self.tables.device_scale_table(dev)
+        dtc = ops.dt_code(hyper)
+        nmax = max(self.stage_sizes(hy, wy))
+        bufs = self._stage_common(hy, wy, B, dev, hyper.dtype)
+
+        def group(gi: int, b0: int, b1: int):
+            nb = b1 - b0
+            idx_pin = self._pinned(f"dec_idx{gi}", nb * nmax)  # sized once: no regrowth mid-loop
+            sym_pin = self._pinned(f"dec_sym{gi}", nb * nmax)
+            sym_dev = torch.empty(nb * nmax, dtype=torch.int32, device=dev)
+
+            def emit(i, phase, params, c, off, yhat_slice, anchor):
+                n = c * hy * (wy // 2)
+                idx = torch.empty((nb, n), dtype=torch.int32, device=dev)
+                ops.call("rdeic_ckbd_indexes", params.data_ptr(), ops.pix_ld(params), nb, hy, wy, c, phase,
+                         table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), idx.data_ptr(), n, 0, dtc,
+                         ops.stream_ptr())
+                idx_p = idx_pin[:nb * n].view(nb, n)
+                sym_p = sym_pin[:nb * n].view(nb, n)
+                sym = sym_dev[:nb * n].view(nb, n)
+                ready = torch.cuda.Event()
+
+                def to_host():
+                    idx_p.copy_(idx, non_blocking=True)
+                    ready.record()
+
+                host_step(to_host)
+                yield  # other groups queue their stages while these indexes come back
+
+                def decode():
+                    ready.synchronize()
+                    coders.rans_decode_batch(self._io["decs"][b0:b1], idx_p.numpy(), self.tables, out=sym_p.numpy())
+                    sym.copy_(sym_p, non_blocking=True)
+
+                host_step(decode)
+                ops.call("rdeic_ckbd_dequant", sym.data_ptr(), params.data_ptr(), ops.pix_ld(params), nb, hy, wy, c,
+                         phase, n, 0, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
+                         None if anchor is None else anchor.data_ptr(), 0 if anchor is None else ops.pix_ld(anchor),
+                         dtc, ops.stream_ptr())
+
+            return self._stage_gen(hyper[b0:b1], hy, wy, emit, [t[b0:b1] for t in bufs])
+
+        self._interleave([group(gi, b0, b1) for gi, (b0, b1) in enumerate(self._groups(B))])
+        guide_hint = self._seq(self.g_s, bufs[0])
+        c_latent = ops.conv2d(guide_hint, self.store.conv(self.p + "out"), out_f32=True)
+        return c_latent, guide_hint
 
     @torch.no_grad()
     def decompress(self, strings_list: Sequence[Sequence[Sequence[bytes]]], shape: Tuple[int, int],
@@ -264,36 +406,20 @@ class Compression:
         B = len(strings_list)
         hz, wz = int(shape[0]), int(shape[1])
         zi = np.stack([coders.ac_decode_uniform(st[1][0], hz * wz, self.codebook_size) for st in strings_list])
-        z_idx = torch.from_numpy(zi.astype(np.int32)).to(device)
-        z_q = self.codebook_entry(z_idx, B, hz, wz)
-        hyper = self._seq(self.hyper_dec, z_q)
-        _, hy, wy, _ = hyper.shape
-        decs = [coders.RansDecoder(st[0][0]) for st in strings_list]
-        nmax = B * max(self.stage_sizes(hy, wy))
-        self._pinned("dec_idx", nmax), self._pinned("dec_sym", nmax)  # size once: no regrowth mid-loop
-        table = self.tables.device_scale_table(hyper.device)
-        dtc = ops.dt_code(hyper)
+        z_idx = torch.from_numpy(zi.astype(np.int32).reshape(B, hz, wz)).to(device)
 
-        def emit(i, phase, params, c, off, yhat_slice, anchor):
-            n = c * hy * (wy // 2)
-            idx = torch.empty((B, n), dtype=torch.int32, device=hyper.device)
-            ops.call("rdeic_ckbd_indexes", params.data_ptr(), ops.pix_ld(params), B, hy, wy, c, phase,
-                     table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), idx.data_ptr(), n, 0, dtc,
-                     ops.stream_ptr())
-            idx_p = self._pinned("dec_idx", B * n).view(B, n)
-            idx_p.copy_(idx, non_blocking=True)
-            torch.cuda.current_stream(hyper.device).synchronize()
-            sym_p = self._pinned("dec_sym", B * n).view(B, n)
-            coders.rans_decode_batch(decs, idx_p.numpy(), self.tables, out=sym_p.numpy())
-            sym = sym_p.to(hyper.device, non_blocking=True)
-            ops.call("rdeic_ckbd_dequant", sym.data_ptr(), params.data_ptr(), ops.pix_ld(params), B, hy, wy, c, phase,
-                     n, 0, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
-                     None if anchor is None else anchor.data_ptr(), 0 if anchor is None else ops.pix_ld(anchor), dtc,
-                     ops.stream_ptr())
+        def fresh_decoders():  # the decoders are stateful: one fresh set per execution of the region
+            for d in self._io.get("decs", []):
+                d.close()
+            self._io["decs"] = [coders.RansDecoder(st[0][0]) for st in strings_list]
 
-        yhat = self._run_stages(hyper, B, hy, wy, emit)
-        for d in decs:
-            d.close()
-        guide_hint = self._seq(self.g_s, yhat)
-        c_latent = ops.conv2d(guide_hint, self.store.conv(self.p + "out"), out_f32=True)
+        self._io = {}
+        try:
+            c_latent, guide_hint = self._run_region("decompress", self._decompress_gpu, [z_idx], before=fresh_decoders)
+            if self.use_plans:  # the plan's outputs are its static buffers
+                c_latent, guide_hint = c_latent.clone(), guide_hint.clone()
+        finally:
+            for d in self._io.get("decs", []):
+                d.close()
+            self._io = {}
         return c_latent, guide_hint

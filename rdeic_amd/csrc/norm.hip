@@ -19,7 +19,18 @@
 
 namespace {
 
-constexpr int GN_CHUNK = 512;  // pixels per pass-1 block
+constexpr int GN_CHUNK_MAX = 512;  // pixels per pass-1 block (fp32; bf16 adapts, gn_chunk)
+
+// Pass-1 pixels per block: 512, halved for bf16 (down to 32) while an image has fewer than 64
+// chunks, so the 64x64 .. 8x8 UNet levels still launch enough blocks to fill the chip. It depends
+// on hw and dtype only, never on the batch, so the statistics stay batch-invariant; the fp32
+// (parity) path keeps 512.
+inline int gn_chunk(int hw, int esize) {
+  int ch = GN_CHUNK_MAX;
+  if (esize == 2)
+    while (ch > 32 && hw / ch < 64) ch >>= 1;
+  return ch;
+}
 
 template <typename T>
 __device__ __forceinline__ float load_seg(const T* x0, int c0, int ld0, const T* x1, int ld1, long img_pix, int ch) {
@@ -29,10 +40,10 @@ __device__ __forceinline__ float load_seg(const T* x0, int c0, int ld0, const T*
 // One segment: channels [coff, coff + cs) of the logical c-channel tensor.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x, int hw, int cs, int ld, int coff,
-                                                         int c, int nchunk, float* __restrict__ part) {
+                                                         int c, int nchunk, int pix_per, float* __restrict__ part) {
   const int img = blockIdx.y, chunk = blockIdx.x;
-  const int p0 = chunk * GN_CHUNK;
-  const int p1 = min(hw, p0 + GN_CHUNK);
+  const int p0 = chunk * pix_per;
+  const int p1 = min(hw, p0 + pix_per);
   const T* xi = x + (long)img * hw * ld;
   int PL = 1;  // pixel lanes when the segment width divides 256
   if (cs < 256 && 256 % cs == 0) PL = 256 / cs;
@@ -75,10 +86,11 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x
 // 16-byte vectorised pass 1 for bf16 (segment width a multiple of 8, at most 2048 channels):
 // thread = one 8-channel chunk of pixels pl, pl+PL, ...; pixel lanes reduced in a fixed order.
 __global__ __launch_bounds__(256) void gn_partial_vec_kernel(const bf16* __restrict__ x, int hw, int cs, int ld,
-                                                             int coff, int c, int nchunk, float* __restrict__ part) {
+                                                             int coff, int c, int nchunk, int pix_per,
+                                                             float* __restrict__ part) {
   const int img = blockIdx.y, chunk = blockIdx.x;
-  const int p0 = chunk * GN_CHUNK;
-  const int p1 = min(hw, p0 + GN_CHUNK);
+  const int p0 = chunk * pix_per;
+  const int p1 = min(hw, p0 + pix_per);
   const bf16* xi = x + (long)img * hw * ld;
   const int cp = cs >> 3;
   const int PL = 256 / cp;
@@ -242,7 +254,10 @@ __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const bf16* __restric
       float4 s = p[q];  // (a, b) of channels ch+2q, ch+2q+1
       float v0 = (float)v[u][2 * q] * s.x + s.y;
       float v1 = (float)v[u][2 * q + 1] * s.z + s.w;
-      if (silu) { v0 = silu_f(v0); v1 = silu_f(v1); }
+      if (silu) {  // x * rcp(1 + e^-x): v_rcp instead of the IEEE divide sequence (bf16 output)
+        v0 *= __builtin_amdgcn_rcpf(1.0f + __expf(-v0));
+        v1 *= __builtin_amdgcn_rcpf(1.0f + __expf(-v1));
+      }
       o[2 * q] = (bf16)(v0 * out_mul);
       o[2 * q + 1] = (bf16)(v1 * out_mul);
     }
@@ -335,15 +350,16 @@ template <typename T>
 int gn_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1, int32_t ld1, int32_t n, int32_t hw,
              int32_t groups, float eps, const float* gamma, const float* beta, float* ab, float* ws, hipStream_t s) {
   const int c = c0 + c1;
-  const int nchunk = (hw + GN_CHUNK - 1) / GN_CHUNK;
+  const int pix_per = gn_chunk(hw, (int)sizeof(T));
+  const int nchunk = (hw + pix_per - 1) / pix_per;
   auto seg = [&](const void* xs, int cs, int ld, int coff) {
     const bool vec = sizeof(T) == 2 && cs % 8 == 0 && cs <= 2048 && ld % 8 == 0 && ((uintptr_t)xs) % 16 == 0;
     if (vec)
       hipLaunchKernelGGL(gn_partial_vec_kernel, dim3(nchunk, n), dim3(256), 0, s, (const bf16*)xs, hw, cs, ld, coff, c,
-                         nchunk, ws);
+                         nchunk, pix_per, ws);
     else
       hipLaunchKernelGGL(gn_partial_kernel<T>, dim3(nchunk, n), dim3(256), 0, s, (const T*)xs, hw, cs, ld, coff, c,
-                         nchunk, ws);
+                         nchunk, pix_per, ws);
   };
   seg(x0, c0, ld0, 0);
   if (c1 > 0) seg(x1, c1, ld1, c0);
@@ -355,7 +371,8 @@ int gn_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1
 }  // namespace
 
 extern "C" size_t rdeic_groupnorm_ws_floats(int32_t n, int32_t hw, int32_t c) {
-  long nchunk = (hw + GN_CHUNK - 1) / GN_CHUNK;
+  const int pix_per = gn_chunk(hw, 2);  // the bf16 chunk is never larger than the fp32 one
+  long nchunk = (hw + pix_per - 1) / pix_per;
   return (size_t)n * nchunk * c * 2;
 }
 

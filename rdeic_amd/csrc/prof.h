@@ -5,11 +5,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-int rdeic_prof_begin(hipStream_t s, int kind);                        // slot, or -1 (off / full / not sampled)
+int rdeic_prof_begin(hipStream_t s, int kind, double work);           // slot, or -1 (off / full / not sampled)
 void rdeic_prof_end(int slot, hipStream_t s, int kind, double work);  // no-op for slot < 0
 
 struct ProfScope {
   int slot; hipStream_t s; int kind; double work;
-  ProfScope(hipStream_t s_, int kind_, double work_) : slot(rdeic_prof_begin(s_, kind_)), s(s_), kind(kind_), work(work_) {}
+  ProfScope(hipStream_t s_, int kind_, double work_)
+      : slot(rdeic_prof_begin(s_, kind_, work_)), s(s_), kind(kind_), work(work_) {}
   ~ProfScope() { rdeic_prof_end(slot, s, kind, work); }
 };

@@ -1,4 +1,10 @@
 // Native launch profiler (see prof.h).
+//
+// Weighted sampling: launches whose algorithmic work is at or above always_threshold(kind) are
+// always timed (weight 1); smaller ones are timed one in g_every (hashed, weight g_every). The
+// read-out is a Horvitz-Thompson estimate: launches = sum w, work = sum w*work, ms = sum w*t.
+// The large launches carry most of the time, so the estimate's variance comes only from the
+// small-launch tail.
 #include <mutex>
 #include <vector>
 
@@ -7,20 +13,26 @@
 #include "../../include/rdeic_hip.h"
 
 namespace {
-struct Slot { hipEvent_t a = nullptr, b = nullptr; int kind = -1; double work = 0.0; };
+struct Slot { hipEvent_t a = nullptr, b = nullptr; int kind = -1; double work = 0.0; double weight = 1.0; };
 std::vector<Slot> g_slots;
 int g_used = 0;
 bool g_on = false;
-int g_every = 1;     // time one launch in g_every (per kind)
+int g_every = 1;     // time one small launch in g_every (per kind)
 long g_seen[8] = {};
 std::mutex g_mu;
+
+double always_threshold(int kind) {
+  // FLOP for the conv / attention kinds, bytes for the GroupNorm kinds
+  return kind <= RDEIC_PROF_ATTN_SMALL ? 50e9 : 64e6;
+}
 }  // namespace
 
-int rdeic_prof_begin(hipStream_t s, int kind) {
+int rdeic_prof_begin(hipStream_t s, int kind, double work) {
   if (!g_on) return -1;
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_on || g_used >= (int)g_slots.size()) return -1;
-  if (kind >= 0 && kind < 8 && g_every > 1) {
+  double weight = 1.0;
+  if (kind >= 0 && kind < 8 && g_every > 1 && work < always_threshold(kind)) {
     // hashed sample (splitmix64 finaliser of the per-kind launch counter): unbiased even when the
     // per-step launch count is a multiple of g_every
     unsigned long long z = (unsigned long long)(g_seen[kind]++) + 0x9E3779B97F4A7C15ull;
@@ -28,9 +40,11 @@ int rdeic_prof_begin(hipStream_t s, int kind) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     z ^= z >> 31;
     if (z % (unsigned long long)g_every != 0) return -1;
+    weight = (double)g_every;
   }
   const int i = g_used++;
   g_slots[i].kind = -1;
+  g_slots[i].weight = weight;
   if (hipEventRecord(g_slots[i].a, s) != hipSuccess) return -1;
   return i;
 }
@@ -48,7 +62,12 @@ extern "C" int rdeic_prof_start(int32_t capacity, int32_t every) {
   std::lock_guard<std::mutex> lk(g_mu);
   while ((int)g_slots.size() < capacity) {
     Slot sl;
-    if (hipEventCreate(&sl.a) != hipSuccess || hipEventCreate(&sl.b) != hipSuccess) return RDEIC_ELAUNCH;
+    // timing-only events: no system-scope fence (no L2 writeback / invalidate per marker, which
+    // otherwise costs the profiled run several % of its step time); callers synchronise the
+    // device before rdeic_prof_read
+    if (hipEventCreateWithFlags(&sl.a, hipEventDisableSystemFence) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.b, hipEventDisableSystemFence) != hipSuccess)
+      return RDEIC_ELAUNCH;
     g_slots.push_back(sl);
   }
   g_used = 0;
@@ -67,14 +86,15 @@ extern "C" int rdeic_prof_stop(void) {
 extern "C" int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms) {
   if (!launches || !work || !ms) return RDEIC_EINVAL;
   std::lock_guard<std::mutex> lk(g_mu);
-  *launches = 0; *work = 0.0; *ms = 0.0;
+  double n = 0.0, w = 0.0, t_ms = 0.0;
   for (int i = 0; i < g_used; ++i) {
     const Slot& sl = g_slots[i];
     if (sl.kind != kind) continue;
     if (hipEventSynchronize(sl.b) != hipSuccess) return RDEIC_ELAUNCH;
     float t = 0.f;
     if (hipEventElapsedTime(&t, sl.a, sl.b) != hipSuccess) return RDEIC_ELAUNCH;
-    *launches += 1; *work += sl.work; *ms += t;
+    n += sl.weight; w += sl.weight * sl.work; t_ms += sl.weight * t;
   }
+  *launches = (int64_t)(n + 0.5); *work = w; *ms = t_ms;
   return RDEIC_OK;
 }

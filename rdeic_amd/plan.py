@@ -14,14 +14,41 @@ launch, so bench.py's HIP events still bracket every conv / attention / GroupNor
 torch refuses timing events inside graph capture: tools/probe/graph_events.py).
 
 Requirements on a recorded region: every GPU operation goes through `_lib.call` (no torch
-kernels: constants are prepared outside), no host synchronisation, fixed shapes. tests/
-test_plan_gpu.py checks replay == eager bit for bit.
+kernels: constants are prepared outside), fixed shapes, and host work (coder round trips,
+pinned copies, event waits) only inside `host_step`, which runs it and records it at its place
+in the sequence: the entropy coder's compress / decompress regions interleave launches with
+host steps. tests/test_plan_gpu.py checks replay == eager bit for bit.
 """
 from __future__ import annotations
 
 import torch
 
 from . import _lib, ops
+
+
+class _HostStep:
+    __slots__ = ("fn",)
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self):
+        self.fn()
+        return 0
+
+
+def host_step(fn) -> None:
+    """Run a host-side step now; inside a recording, also append it to the plan so replay() runs
+    it at the same point of the launch sequence. Library calls made by the step itself (the
+    rANS coders) belong to the step and are not recorded as launches."""
+    rec = _lib.RECORDER
+    if rec is not None:
+        rec.append(("<host>", _HostStep(fn), (), None))
+    _lib.RECORDER = None
+    try:
+        fn()
+    finally:
+        _lib.RECORDER = rec
 
 
 class LaunchPlan:
@@ -66,15 +93,23 @@ class PlanCache:
     def __init__(self):
         self.plans = {}
 
-    def run(self, key, fn, inputs):
+    def run(self, key, fn, inputs, before=None):
+        """before(): resets per-call host state (e.g. reopens the rANS decoders) ahead of each
+        execution of the region: the warm-up, the recording and every replay."""
         ent = self.plans.get(key)
         if ent is None:
             statics = [t.clone() for t in inputs]
+            if before is not None:
+                before()
             fn(*statics)  # eager warm-up: autotune caches, packed weights, split-K workspace
             plan = LaunchPlan()
+            if before is not None:
+                before()
             out = plan.record(fn, *statics)
             self.plans[key] = (plan, statics)
             return out
+        if before is not None:
+            before()
         plan, statics = ent
         for s, t in zip(statics, inputs):
             if s.data_ptr() != t.data_ptr():

@@ -79,17 +79,30 @@ class RDEIC:
         """Synthetic weights (rdeic_amd/weights.py); rate_gain is the bpp knob (weights.RATE_LAYERS)."""
         from . import weights as W
         self.store.init_synthetic(W.GLOBAL_SEED if seed is None else seed, rate_gain)
-        self._plans.clear()  # recorded plans point at the previous packed weights
-        self.preprocess_model._en = None
+        self._clear_plans()  # recorded plans point at the previous packed weights
         return self
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
         """Load reference-named weights (e.g. a RDEIC checkpoint's state_dict). Non-parameter buffers of the
         reference (schedules, entropy tables, scale_list, cond_stage_model) are ignored."""
         self.store.load_state_dict({k: v for k, v in sd.items() if k in self.store.shapes}, strict=strict)
-        self._plans.clear()
-        self.preprocess_model._en = None
+        self._clear_plans()
         return self
+
+    @property
+    def use_plans(self) -> bool:
+        return self._use_plans
+
+    @use_plans.setter
+    def use_plans(self, v: bool):
+        """Launch-plan replay for every fixed-shape region (compress, decompress, relay + decode)."""
+        self._use_plans = bool(v)
+        self.preprocess_model.use_plans = bool(v)
+
+    def _clear_plans(self):
+        self._plans.clear()
+        self.preprocess_model._plans.clear()
+        self.preprocess_model._en = None
 
     def param_shapes(self):
         return dict(self.store.shapes)
@@ -185,8 +198,9 @@ class RDEIC:
     @torch.no_grad()
     def compress_images(self, img_u8: torch.Tensor) -> List[bytes]:
         """uint8 [B,H,W,3] (H, W multiples of 64) -> B bitstream bodies (reference file format)."""
-        h = self.encode_images_nhwc(img_u8.to(self.device))
-        return [bitstream.pack_body(o["shape"], o["strings"]) for o in self.preprocess_model.compress(h)]
+        img = img_u8.to(self.device).contiguous()
+        outs = self.preprocess_model.compress_with(self.encode_images_nhwc, img)  # VAE encoder in the same plan
+        return [bitstream.pack_body(o["shape"], o["strings"]) for o in outs]
 
     @torch.no_grad()
     def decompress_bodies(self, bodies: Sequence[bytes]):
