@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=16, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=512)
-    ap.add_argument("--ddim-steps", type=int, default=2)
+    ap.add_argument("--ddim-steps", type=int, default=2, help="relay sampler steps")
+    ap.add_argument("--sampler", default="ddim", choices=["ddim", "ddpm"],
+                    help="relay sampler (config 2 names 2-step relay DDIM; ddpm = the CLI's spaced sampler)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -70,7 +72,7 @@ def main():
     args = parse()
     from rdeic_amd import ops, parallel
     from rdeic_amd.rdeic import RDEIC
-    from rdeic_amd.synthetic import sampler_noise, synth_context, synth_image
+    from rdeic_amd.synthetic import relay_noise, synth_context, synth_image
 
     rank, world, local = parallel.init_from_env()
     dev = torch.device("cuda", local)
@@ -88,12 +90,15 @@ def main():
 
     g0 = rank * B  # global image indices of this rank's shard (weak scaling: B per GPU)
     imgs = torch.from_numpy(np.stack([synth_image(S, S, 231 + g0 + i) for i in range(B)])).to(dev)
-    noise = torch.cat([sampler_noise((1, 4, S // 8, S // 8), 231 + g0 + i)[1] for i in range(B)])
+    draws = [relay_noise((1, 4, S // 8, S // 8), 231 + g0 + i, args.ddim_steps) for i in range(B)]
+    noise = torch.cat([d[0] for d in draws])
+    step_noise = torch.cat([d[1] for d in draws], 1) if args.sampler == "ddpm" else None
     ctx = synth_context().to(dev)
     mse = torch.empty(B, dtype=torch.float32, device=dev)
 
     def step():
-        out, bodies = model.codec_images(imgs, ctx, noise, steps=args.ddim_steps)
+        out, bodies = model.codec_images(imgs, ctx, noise, steps=args.ddim_steps, sampler=args.sampler,
+                                         step_noise_nchw=step_noise)
         ops.call("rdeic_image_mse", imgs.data_ptr(), out.data_ptr(), B, S * S * 3, mse.data_ptr(), ops.stream_ptr())
         m = mse.cpu().numpy()
         rows = torch.tensor([[len(b) * 8.0 / (S * S), float(len(b)),
@@ -165,9 +170,10 @@ def main():
         "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded images, random-init weights)",
-        "config": {"workload": f"config 2: batch {B}/GPU {S}x{S}, {args.ddim_steps}-step relay DDIM, "
+        "config": {"workload": f"config 2: batch {B}/GPU {S}x{S}, {args.ddim_steps}-step relay "
+                               f"{'DDIM' if args.sampler == 'ddim' else 'spaced DDPM'}, "
                                f"encode+entropy-code+decode+VAE-decode", "global_batch": B * world,
-                   "image_size": S, "ddim_steps": args.ddim_steps, "parallelism": f"dp{world}", "rate_gain": rate_gain,
+                   "image_size": S, "ddim_steps": args.ddim_steps, "sampler": args.sampler, "parallelism": f"dp{world}", "rate_gain": rate_gain,
                    "mean_bpp": round(float(mrows[:, 0].mean()), 4),
                    "mean_psnr_db": round(float(mrows[:, 2].mean()), 2)},
         "roofline": roof,

@@ -154,6 +154,12 @@ int rdeic_timestep_embedding(const int64_t* t, const float* freqs, int32_t n, in
 /* relay-DDIM eta=0 update (ddim_sampler_relay.py:215-229) with host-precomputed fp32 scalars */
 int rdeic_ddim_step(const float* x, const float* e, int64_t count, float c_sq1m, float c_sqa, float c_sqap,
                     float c_dir, float* xp, float* x0, void* stream);
+/* relay spaced (DDPM) update (spaced_sampler_relay.py:270-275 _predict_xstart_from_eps, :154-170
+ * q_posterior_mean_variance, :378-383 x_prev): pred_x0 = a*x - b*e, mean = c1*pred_x0 + c2*x,
+ * xp = mean + s*noise (s = nonzero_mask * sqrt(model_variance)); fp32 scalars from the host's
+ * float64 schedule; noise may be NULL only when s == 0; x0 (pred_x0 out) may be NULL. */
+int rdeic_spaced_step(const float* x, const float* e, const float* noise, int64_t count, float a, float b, float c1,
+                      float c2, float s, float* xp, float* x0, void* stream);
 /* SiLU in place / copy (fp32), for embedding MLP inputs */
 int rdeic_silu_f32(const float* x, float* y, int64_t count, void* stream);
 /* image u8 HWC <-> model tensors (inference.py:51-52, 85-87) */

@@ -8,7 +8,8 @@ Differences from the reference, all forced by the offline image:
   * no checkpoint is shipped: without --ckpt the model uses the seeded synthetic weights;
     with --ckpt, a plain state dict is read with torch.load(weights_only=True);
   * the OpenCLIP "" embedding (reference :122) is replaced by the seeded synthetic context;
-  * only --sampler ddim is available (the SpacedSampler "ddpm" default is SURVEY §8f rank 3).
+  * the noise draws (x_T, q_sample noise, and the spaced sampler's per-step randn_like) come from a
+    seeded CPU generator in the reference's order, not from the device RNG.
 The noise draws follow the reference order (inference.py:64-65: a discarded randn, then noise).
 """
 import os
@@ -45,8 +46,7 @@ def process(model, imgs: List[np.ndarray], sampler: str, steps: int, stream_path
             c_crossattn: List[torch.Tensor], generator: torch.Generator) -> Tuple[List[np.ndarray], float]:
     """reference inference.py:22-91 on the HIP path."""
     from rdeic_amd.ddim_sampler_relay import DDIMSampler
-    if sampler != "ddim":
-        raise NotImplementedError("only the relay DDIM sampler is implemented (use --sampler ddim)")
+    from rdeic_amd.spaced_sampler_relay import SpacedSampler
     n = len(imgs)
     control = torch.tensor(np.stack(imgs) / 255.0, dtype=torch.float32).clamp_(0, 1)
     control = control.permute(0, 3, 1, 2).contiguous().to(model.device)
@@ -59,9 +59,15 @@ def process(model, imgs: List[np.ndarray], sampler: str, steps: int, stream_path
     noise = torch.randn(shape, generator=generator).to(model.device)
     t = torch.full((n,), model.used_timesteps - 1, dtype=torch.long, device=model.device)
     x_T = model.q_sample(x_start=c_latent, t=t, noise=noise)
-    samples, _ = DDIMSampler(model).sample(S=steps, batch_size=n, shape=shape[1:], conditioning=cond,
-                                           unconditional_conditioning=None,
-                                           unconditional_guidance_scale=guidance_scale, x_T=x_T, eta=0)
+    if sampler == "ddpm":
+        step_noise = [torch.randn(shape, generator=generator) for _ in range(steps)]
+        samples = SpacedSampler(model, var_type="fixed_small").sample(
+            steps, shape, cond, unconditional_guidance_scale=guidance_scale, unconditional_conditioning=None,
+            cond_fn=None, x_T=x_T, step_noise=step_noise)
+    else:
+        samples, _ = DDIMSampler(model).sample(S=steps, batch_size=n, shape=shape[1:], conditioning=cond,
+                                               unconditional_conditioning=None,
+                                               unconditional_guidance_scale=guidance_scale, x_T=x_T, eta=0)
     x = model.decode_first_stage(samples)
     x = ((x + 1) / 2).clamp(0, 1)
     x = (x.permute(0, 2, 3, 1) * 255).cpu().numpy().clip(0, 255).astype(np.uint8)
@@ -73,7 +79,7 @@ def parse_args(argv=None) -> Namespace:
     p.add_argument("--ckpt", default="", type=str, help="state dict (.pt/.ckpt, tensors only); empty = synthetic")
     p.add_argument("--config", default="", type=str, help="accepted for compatibility (architecture is fixed)")
     p.add_argument("--input", type=str, required=True)
-    p.add_argument("--sampler", type=str, default="ddim", choices=["ddpm", "ddim"])
+    p.add_argument("--sampler", type=str, default="ddpm", choices=["ddpm", "ddim"])
     p.add_argument("--steps", default=2, type=int)
     p.add_argument("--guidance_scale", default=1.0, type=float)
     p.add_argument("--output", type=str, default="results/")

@@ -1,7 +1,8 @@
 // Elementwise / layout kernels on the RDEIC hot path (gfx950).
 //   * GEGLU gate (attention.py:49-56)
 //   * NCHW fp32 <-> internal NHWC conversions at the API boundary
-//   * q_sample and the relay-DDIM update (ddpm.py:357-360, ddim_sampler_relay.py:203-231)
+//   * q_sample, the relay-DDIM update (ddpm.py:357-360, ddim_sampler_relay.py:203-231) and the relay
+//     spaced-sampler update (spaced_sampler_relay.py:154-170,270-275,349-384)
 //   * sinusoidal timestep embedding (util.py:161-181)
 //   * uint8 image <-> model tensors (inference.py:51-52, 85-87)
 //   * counter-based synthetic weights and weight packing for the implicit-GEMM conv
@@ -70,6 +71,20 @@ __global__ void ddim_step_kernel(const float* __restrict__ x, const float* __res
     float p = __fdiv_rn(__fsub_rn(x[i], __fmul_rn(c_sq1m, e[i])), c_sqa);
     if (x0) x0[i] = p;
     xp[i] = __fadd_rn(__fmul_rn(c_sqap, p), __fmul_rn(c_dir, e[i]));
+  }
+}
+
+// Spaced (DDPM) update in the reference's op order, every product and sum rounded on its own:
+//   pred_x0 = A * x - B * e;   mean = C1 * pred_x0 + C2 * x;   x' = mean + S * noise
+__global__ void spaced_step_kernel(const float* __restrict__ x, const float* __restrict__ e,
+                                   const float* __restrict__ noise, long count, float A, float B, float C1, float C2,
+                                   float S, float* __restrict__ xp, float* __restrict__ x0) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    const float xv = x[i];
+    const float p = __fsub_rn(__fmul_rn(A, xv), __fmul_rn(B, e[i]));
+    if (x0) x0[i] = p;
+    const float mean = __fadd_rn(__fmul_rn(C1, p), __fmul_rn(C2, xv));
+    xp[i] = noise ? __fadd_rn(mean, __fmul_rn(S, noise[i])) : mean;
   }
 }
 
@@ -213,6 +228,14 @@ extern "C" int rdeic_ddim_step(const float* x, const float* e, int64_t count, fl
   if (!x || !e || !xp || count <= 0) return RDEIC_EINVAL;
   hipLaunchKernelGGL(ddim_step_kernel, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream, x, e, (long)count,
                      c_sq1m, c_sqa, c_sqap, c_dir, xp, x0);
+  return launch_status();
+}
+
+extern "C" int rdeic_spaced_step(const float* x, const float* e, const float* noise, int64_t count, float a,
+                                 float b, float c1, float c2, float s, float* xp, float* x0, void* stream) {
+  if (!x || !e || !xp || count <= 0 || (!noise && s != 0.f)) return RDEIC_EINVAL;
+  hipLaunchKernelGGL(spaced_step_kernel, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream, x, e, noise,
+                     (long)count, a, b, c1, c2, s, xp, x0);
   return launch_status();
 }
 

@@ -59,6 +59,7 @@ class RDEIC:
         self.scale_factor = float(cfg["scale_factor"])
         self.num_timesteps = int(cfg["timesteps"])
         self.used_timesteps = int(cfg["used_timesteps"])
+        self.linear_start, self.linear_end = float(cfg["linear_start"]), float(cfg["linear_end"])
         self.channels = 4
         sched = make_schedule(self.num_timesteps, cfg["linear_start"], cfg["linear_end"])
         self._sched_cpu = sched
@@ -210,62 +211,98 @@ class RDEIC:
             raise ValueError("batched decompress needs one latent shape per batch")
         return self.preprocess_model.decompress([p[0] for p in parsed], shape, device=self.device)
 
+    @staticmethod
+    def _sampler(model, sampler: str):
+        if sampler == "ddim":
+            from .ddim_sampler_relay import DDIMSampler
+            return DDIMSampler(model)
+        if sampler == "ddpm":
+            from .spaced_sampler_relay import SpacedSampler
+            return SpacedSampler(model, var_type="fixed_small")  # inference.py:47-48
+        raise ValueError(f"sampler {sampler!r} (ddpm | ddim)")
+
+    def _step_timesteps(self, steps: int, sampler: str):
+        if sampler == "ddpm":
+            from .spaced_sampler_relay import space_timesteps
+            return sorted(space_timesteps(self.used_timesteps, str(steps)))
+        from .ddim_sampler_relay import make_ddim_timesteps
+        return [int(t) for t in make_ddim_timesteps(steps, self.used_timesteps)]
+
     @torch.no_grad()
     def relay_sample_nhwc(self, c_latent: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor,
-                          noise: torch.Tensor, steps: int) -> torch.Tensor:
-        """x_T = q_sample(c_latent, used_timesteps-1, noise); relay DDIM (eta=0) for `steps` steps."""
-        from .ddim_sampler_relay import DDIMSampler
+                          noise: torch.Tensor, steps: int, sampler: str = "ddim", step_noise=None) -> torch.Tensor:
+        """x_T = q_sample(c_latent, used_timesteps-1, noise); relay DDIM (eta=0) or spaced DDPM sampling."""
         B = c_latent.shape[0]
         t = torch.full((B,), self.used_timesteps - 1, dtype=torch.long, device=self.device)
         x = self.q_sample_nhwc(c_latent, t, noise)
-        return DDIMSampler(self).sample_nhwc(steps, x, guide_hint, context)
+        if sampler == "ddpm":
+            return self._sampler(self, sampler).sample_nhwc(steps, x, guide_hint, context, step_noise=step_noise)
+        return self._sampler(self, sampler).sample_nhwc(steps, x, guide_hint, context)
 
-    def _region_consts(self, B: int, steps: int, device) -> dict:
-        """Per-(batch, steps) device constants of the relay + decode region, made outside any
-        recorded launch plan (a plan replays only librdeic_hip launches)."""
-        key = (B, steps, str(device))
+    def _region_consts(self, B: int, steps: int, device, sampler: str = "ddim") -> dict:
+        """Per-(batch, steps, sampler) device constants of the relay + decode region, made outside
+        any recorded launch plan (a plan replays only librdeic_hip launches)."""
+        key = (B, steps, str(device), sampler)
         c = self._consts.get(key)
         if c is None:
-            from .ddim_sampler_relay import make_ddim_timesteps
             t = torch.full((B,), self.used_timesteps - 1, dtype=torch.long, device=device)
             c = {"qa": self.sqrt_alphas_cumprod[t].contiguous(), "qb": self.sqrt_one_minus_alphas_cumprod[t].contiguous(),
                  "inv_scale": torch.full((B,), 1.0 / self.scale_factor, dtype=torch.float32, device=device),
                  "zero": torch.zeros((B,), dtype=torch.float32, device=device), "ts": {}}
             if steps:
-                for st in make_ddim_timesteps(steps, self.used_timesteps):
+                for st in self._step_timesteps(steps, sampler):
                     c["ts"][int(st)] = torch.full((B,), int(st), dtype=torch.long, device=device)
             self._consts[key] = c
         return c
 
-    def _relay_decode_u8(self, c_latent, guide_hint, context, noise, steps: int):
-        """q_sample(c_latent, 299, noise) -> relay DDIM -> VAE decode -> uint8 NHWC (launches only)."""
-        from .ddim_sampler_relay import DDIMSampler
+    def _relay_decode_u8(self, c_latent, guide_hint, context, noise, steps: int, sampler: str = "ddim",
+                         step_noise=None):
+        """q_sample(c_latent, 299, noise) -> relay sampler -> VAE decode -> uint8 NHWC (launches only).
+        step_noise: [steps, B, h, w, 4] fp32 (ddpm only)."""
         B = c_latent.shape[0]
-        c = self._region_consts(B, steps, c_latent.device)
+        c = self._region_consts(B, steps, c_latent.device, sampler)
         x = torch.empty_like(c_latent)
         ops.call("rdeic_axpby", c_latent.data_ptr(), noise.data_ptr(), B, c_latent[0].numel(), c["qa"].data_ptr(),
                  c["qb"].data_ptr(), x.data_ptr(), ops.stream_ptr())
-        z = DDIMSampler(self).sample_nhwc(steps, x, guide_hint, context, ts_tensors=c["ts"])
+        smp = self._sampler(self, sampler)
+        if sampler == "ddpm":
+            z = smp.sample_nhwc(steps, x, guide_hint, context, step_noise=list(step_noise.unbind(0)),
+                                ts_tensors=c["ts"])
+        else:
+            z = smp.sample_nhwc(steps, x, guide_hint, context, ts_tensors=c["ts"])
         return self.to_image_u8(self.decode_nhwc(z, out_f32=True, consts=c))
 
     @torch.no_grad()
     def relay_decode_u8(self, c_latent: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor,
-                        noise: torch.Tensor, steps: int) -> torch.Tensor:
+                        noise: torch.Tensor, steps: int, sampler: str = "ddim", step_noise=None) -> torch.Tensor:
         """Relay denoise + VAE decode of a batch to uint8 [B,H,W,3]. With use_plans (default) the
         fixed-shape launch sequence is recorded once per shape and replayed (rdeic_amd/plan.py);
-        the result is bit-identical to the eager path."""
+        the result is bit-identical to the eager path. sampler "ddpm" (the reference CLI default)
+        needs step_noise [steps, B, h, w, 4] fp32 NHWC (the per-step randn_like draws)."""
         ctx = context.to(device=self.device, dtype=self.compute_dtype).contiguous()
         ins = [c_latent.contiguous(), guide_hint.contiguous(), ctx, noise.contiguous()]
+        if sampler == "ddpm":
+            if step_noise is None or tuple(step_noise.shape) != (steps,) + tuple(noise.shape):
+                raise ValueError("sampler 'ddpm' needs step_noise of shape [steps, *noise.shape]")
+            ins.append(step_noise.to(device=self.device, dtype=torch.float32).contiguous())
+        elif sampler != "ddim":
+            raise ValueError(f"sampler {sampler!r} (ddpm | ddim)")
+        fn = (lambda a, b, c, d, *e: self._relay_decode_u8(a, b, c, d, steps, sampler, e[0] if e else None))
         if not self.use_plans:
-            return self._relay_decode_u8(*ins, steps)
-        key = ("relay_decode", steps) + tuple((tuple(t.shape), t.dtype) for t in ins)
-        return self._plans.run(key, lambda a, b, c, d: self._relay_decode_u8(a, b, c, d, steps), ins).clone()
+            return fn(*ins)
+        key = ("relay_decode", steps, sampler) + tuple((tuple(t.shape), t.dtype) for t in ins)
+        return self._plans.run(key, fn, ins).clone()
 
     @torch.no_grad()
-    def codec_images(self, img_u8: torch.Tensor, context: torch.Tensor, noise_nchw: torch.Tensor, steps: int = 2):
+    def codec_images(self, img_u8: torch.Tensor, context: torch.Tensor, noise_nchw: torch.Tensor, steps: int = 2,
+                     sampler: str = "ddim", step_noise_nchw: Optional[torch.Tensor] = None):
         """The full hot path on a batch: compress -> bytes -> decompress -> relay denoise -> VAE decode -> u8.
-        Returns (uint8 [B,H,W,3] on device, list of bitstream bodies)."""
+        step_noise_nchw: [steps, B, 4, h, w] (sampler "ddpm"). Returns (uint8 [B,H,W,3] on device, bodies)."""
         bodies = self.compress_images(img_u8)
         c_lat, hint = self.decompress_bodies(bodies)
         noise = ops.nchw_to_nhwc(noise_nchw.float().to(self.device), torch.float32)
-        return self.relay_decode_u8(c_lat, hint, context, noise, steps), bodies
+        step_noise = None
+        if step_noise_nchw is not None:
+            step_noise = torch.stack([ops.nchw_to_nhwc(n.float().to(self.device), torch.float32)
+                                      for n in step_noise_nchw])
+        return self.relay_decode_u8(c_lat, hint, context, noise, steps, sampler, step_noise), bodies

@@ -29,3 +29,13 @@ def sampler_noise(shape, seed: int):
     discarded = torch.randn(shape, generator=g)
     noise = torch.randn(shape, generator=g)
     return discarded, noise
+
+
+def relay_noise(shape, seed: int, steps: int):
+    """(noise, step_noise [steps, *shape]) from one CPU generator in the reference's draw order for
+    `--sampler ddpm`: the discarded x_T randn, the q_sample noise (inference.py:64-65), then one
+    randn_like per sampler step (spaced_sampler_relay.py:378)."""
+    g = torch.Generator().manual_seed(int(seed))
+    torch.randn(shape, generator=g)
+    noise = torch.randn(shape, generator=g)
+    return noise, torch.stack([torch.randn(shape, generator=g) for _ in range(steps)])

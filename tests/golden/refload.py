@@ -147,6 +147,7 @@ def load():
     xformers_state.disable_xformers()
     import model.compression as compression
     import model.ddim_sampler_relay as ddim_mod
+    import model.spaced_sampler_relay as spaced_mod
     import utils.ckbd as ckbd
 
     # AST-extract NoiseEstimator & co. from model/rdeic.py (its module imports pyiqa / PL)
@@ -168,5 +169,6 @@ def load():
         Decoder=vae_model.Decoder, ResnetBlock=vae_model.ResnetBlock, AttnBlock=vae_model.AttnBlock,
         SpatialTransformer=attention.SpatialTransformer, UNetResBlock=openaimodel.ResBlock,
         Compression=compression.Compression, DDIMSampler=ddim_mod.DDIMSampler, ckbd=ckbd, util=util,
+        SpacedSampler=spaced_mod.SpacedSampler, space_timesteps=spaced_mod.space_timesteps,
         timestep_embedding=util.timestep_embedding)
     return _loaded

@@ -17,11 +17,29 @@ def test_cli_matches_golden(tmp_path):
     src = tmp_path / "in"
     src.mkdir()
     Image.fromarray(g["img0_in"]).save(src / "kodim.png")
-    inference.main(["--input", str(src), "--output", str(tmp_path / "out"), "--steps", "2", "--seed", "231"])
+    inference.main(["--input", str(src), "--output", str(tmp_path / "out"), "--steps", "2", "--seed", "231",
+                    "--sampler", "ddim"])
     data = (tmp_path / "out" / "data" / "kodim").read_bytes()
     assert data == g["img0_file"].tobytes()
     out = np.array(Image.open(tmp_path / "out" / "kodim.png"))
     assert np.abs(out.astype(int) - g["img0_image_out"][0].astype(int)).max() <= 1
+
+
+@pytest.mark.gpu
+def test_cli_default_ddpm_sampler(tmp_path):
+    """The reference CLI's default sampler (--sampler ddpm): the bitstream is sampler-independent
+    (golden bytes), the reconstruction comes from the spaced sampler (differs from the DDIM one)."""
+    from PIL import Image
+    import inference
+    g = np.load(GOLDEN)
+    src = tmp_path / "in"
+    src.mkdir()
+    Image.fromarray(g["img0_in"]).save(src / "kodim.png")
+    inference.main(["--input", str(src), "--output", str(tmp_path / "out"), "--steps", "2", "--seed", "231"])
+    assert (tmp_path / "out" / "data" / "kodim").read_bytes() == g["img0_file"].tobytes()
+    out = np.array(Image.open(tmp_path / "out" / "kodim.png"))
+    assert out.shape == g["img0_image_out"][0].shape
+    assert np.abs(out.astype(int) - g["img0_image_out"][0].astype(int)).max() > 1
 
 
 def test_pad_matches_reference_rule():
