@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--coder-groups", type=int, default=None,
                     help="image groups interleaved in the entropy-stage loops (default: the library's)")
     ap.add_argument("--no-plans", action="store_true", help="eager launches (no launch-plan replay), A/B only")
+    ap.add_argument("--no-geglu-fuse", action="store_true", help="unfused GEGLU (projection + geglu kernel), A/B only")
     ap.add_argument("--rate-gain", type=float, default=None,
                     help="synthetic bpp knob (rdeic_amd/weights.py); default: the ~0.08 bpp gain of config 2")
     return ap.parse_args()
@@ -87,6 +88,8 @@ def main():
         model.preprocess_model.coder_groups = args.coder_groups
     if args.no_plans:
         model.use_plans = False
+    if args.no_geglu_fuse:
+        ops.GEGLU_FUSED = False
 
     g0 = rank * B  # global image indices of this rank's shard (weak scaling: B per GPU)
     imgs = torch.from_numpy(np.stack([synth_image(S, S, 231 + g0 + i) for i in range(B)])).to(dev)

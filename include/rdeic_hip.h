@@ -64,7 +64,9 @@ typedef struct rdeic_conv_desc {
   int32_t res_ld;
   void* out;
   int32_t out_ld;       /* pixel stride of out (elements) */
-  int32_t out_mode;     /* 0 NHWC, 1 fused PixelShuffle(2): out is [n][2ho][2wo][cout/4] */
+  int32_t out_mode;     /* 0 NHWC, 1 fused PixelShuffle(2): out is [n][2ho][2wo][cout/4],
+                           2 fused GEGLU (attention.py:49-56): weight rows interleaved as 4 value / 4 gate,
+                           out[p][cout/2] = x * gelu_erf(gate); bf16, LDS-DMA-eligible shapes, no res/emb/act */
   int32_t dtype;        /* 0 fp32 (parity mode), 1 bf16 (fp32 accumulate) */
   int32_t out_f32;      /* bf16 mode only: write fp32 output (and read fp32 residual) */
   int32_t batch;        /* >1: batched GEMM (grid z); operand z starts at +z*{in,w,out}_bs elements */

@@ -112,9 +112,9 @@ __device__ __forceinline__ uint4 gn_apply_chunk(uint4 raw, const float* ab, int 
 // ((acc + bias) + emb -> act -> + res -> round), so results are bit-identical to it.
 // Needs BM/2 * (BN + 4) * 4 bytes of LDS; the caller has finished with its k-loop buffers.
 __device__ __forceinline__ bool epi_vec_ok(const ConvArgs& a) {
-  const bool of32 = a.out_f32;
+  if (a.out_mode == 2) return (a.cout % 8) == 0 && (a.out_ld % 4) == 0 && ((uintptr_t)a.out % 8) == 0;
   return a.out_mode == 0 && (a.cout % 8) == 0 && (a.out_ld % 8) == 0 && ((uintptr_t)a.out % 16) == 0 &&
-         (!a.res || ((a.res_ld % 8) == 0 && ((uintptr_t)a.res % 16) == 0)) && (!of32 || true);
+         (!a.res || ((a.res_ld % 8) == 0 && ((uintptr_t)a.res % 16) == 0));
 }
 
 template <int BM, int BN, int WGM, int WGN, int NT, int P = 2>
@@ -165,6 +165,20 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act, a.act_param);
+      if (a.out_mode == 2) {
+        // fused GEGLU (attention.py:49-56): the packed weight interleaves 4 value rows with their 4
+        // gate rows, so this chunk is (x0..x3, g0..g3) of output channels nn/2 .. nn/2+3. Both halves
+        // are rounded to bf16 first, as the unfused projection + rdeic_geglu see them.
+        bf16 gv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xv = to_f32(from_f32<bf16>(v[e])), gt = to_f32(from_f32<bf16>(v[4 + e]));
+          gv[e] = from_f32<bf16>(xv * gelu_f(gt));
+        }
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + (nn >> 1)) =
+            *reinterpret_cast<uint2*>(gv);
+        continue;
+      }
       if (a.res) {
         if (of32) {
           const float4 r0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.res) + (long)m * a.res_ld + nn);
@@ -879,11 +893,12 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_dma_kernel(ConvArgs a, in
   }
 
   if constexpr (TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * STAGE) {
-    if (a.epi_vec && epi_vec_ok(a)) {
+    if ((a.epi_vec || a.out_mode == 2) && epi_vec_ok(a)) {
       epilogue_vec<BM, BN, WGM, WGN, NT, EP>(acc, a, m0, n0, wm, wn, lane, tid, lds);
       return;
     }
   }
+  if (a.out_mode == 2) return;  // unreachable: the host admits GEGLU only where the vector epilogue runs
   const bool of32 = a.out_f32;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -1059,7 +1074,11 @@ int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec) {
   const int BK = d->dtype == 1 ? 64 : 32;
   if (d->wld < a.ktot || d->wld % 64 != 0) return RDEIC_EINVAL;
   a.nk = (a.ktot + BK - 1) / BK;
+  if (d->out_mode < 0 || d->out_mode > 2) return RDEIC_EINVAL;
   if (d->out_mode == 1 && (d->cout % 4 != 0)) return RDEIC_EINVAL;
+  if (d->out_mode == 2 && (d->dtype != 1 || d->cout % 8 || d->res || d->emb || d->act || d->out_f32 || d->gn_ab ||
+                           a.batch > 1 || d->out_ld % 4 || ((uintptr_t)d->out) % 8))
+    return RDEIC_EINVAL;
   const int epc = d->dtype == 1 ? 8 : 4;
   vec = (d->c0 % epc == 0) && (d->ld0 % epc == 0) && (((uintptr_t)d->in0) % 16 == 0);
   if (d->c1) vec = vec && (d->c1 % epc == 0) && (d->ld1 % epc == 0) && (((uintptr_t)d->in1) % 16 == 0);
@@ -1074,6 +1093,10 @@ static int conv2d_impl(const rdeic_conv_desc* d, void* stream) {
   const int rc = make_args(d, a, vec);
   if (rc != RDEIC_OK) return rc;
   hipStream_t s = (hipStream_t)stream;
+  if (d->out_mode == 2) {  // fused GEGLU exists in the LDS-DMA kernel's vector epilogue only
+    const int rc2 = vec ? dma_grouped(d, -1, 1, nullptr, s) : -1;
+    return rc2 == -1 ? RDEIC_EINVAL : rc2;
+  }
 
   if (d->dtype == 1 && vec && d->cout <= 4 && d->c0 % 32 == 0 && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad_t == 1 &&
       d->pad_l == 1 && !d->up2 && !d->c1 && d->out_mode == 0 && a.batch == 1 && d->ho == d->h && d->wo == d->w &&
@@ -1106,6 +1129,10 @@ static int conv2d_tile_impl(const rdeic_conv_desc* d, int32_t tile, void* stream
   bool vec = false;
   const int rc = make_args(d, a, vec);
   if (rc != RDEIC_OK) return rc;
+  if (d->out_mode == 2) {
+    const int rc2 = vec ? dma_grouped(d, tile >= 20 ? tile : -1, 1, nullptr, (hipStream_t)stream) : -1;
+    return rc2 == -1 ? RDEIC_EINVAL : rc2;
+  }
   if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path != 0) {
     if (tile >= 20) {
       const int rc2 = dma_grouped(d, tile, 1, nullptr, (hipStream_t)stream);

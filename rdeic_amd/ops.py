@@ -86,8 +86,10 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
            pad_t: Optional[int] = None, pad_l: Optional[int] = None, out_hw=None,
            gn: Optional[torch.Tensor] = None, gn_silu: bool = False, emb: Optional[torch.Tensor] = None,
            act: int = NONE, slope: float = 0.0, res: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False) -> torch.Tensor:
-    """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC)."""
+           out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False,
+           geglu: bool = False) -> torch.Tensor:
+    """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC).
+    geglu: p packed by ParamStore.conv_geglu; out = value * gelu(gate), cout/2 channels (bf16)."""
     if gn is not None and _gn_materialize(x, x2, p):
         # the big-tile conv path has no GroupNorm prologue (it is VALU-bound there): materialise the
         # normalised (concatenated) input once with the vectorised, HBM-rate apply kernel instead
@@ -118,7 +120,12 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     else:
         ho, wo = out_hw
     odt = torch.float32 if (out_f32 or x.dtype == torch.float32) else x.dtype
-    if pixel_shuffle:
+    if geglu:
+        if x.dtype != torch.bfloat16 or c0 % 64 or c1 % 64 or p.cout % 8 or res is not None or emb is not None \
+                or act != NONE or out_f32 or pixel_shuffle:
+            raise ValueError("fused GEGLU: bf16, 64-channel-aligned input, no residual / emb / activation")
+        oshape = (n, ho, wo, p.cout // 2)
+    elif pixel_shuffle:
         oshape = (n, 2 * ho, 2 * wo, p.cout // 4)
     else:
         oshape = (n, ho, wo, p.cout)
@@ -152,16 +159,16 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
         d.res_ld = pix_ld(res)
     d.out = out.data_ptr()
     d.out_ld = pix_ld(out)
-    d.out_mode = 1 if pixel_shuffle else 0
+    d.out_mode = 2 if geglu else (1 if pixel_shuffle else 0)
     d.dtype = dt_code(x)
     d.out_f32 = int(odt == torch.float32 and x.dtype != torch.float32)
     d.batch = 1
     flops = 2.0 * n * ho * wo * p.cout * p.kh * p.kw * p.cin
-    splits = _splitk_count(x, x2, n * ho * wo, p, gn is not None or pixel_shuffle, out)
+    splits = _splitk_count(x, x2, n * ho * wo, p, gn is not None or pixel_shuffle or geglu, out)
 
     tile = -1
     if splits == 1 and AUTOTUNE and gn is None and _gn_materialize(x, x2, p):
-        key = (n * ho * wo, p.cout, p.kh, p.kw, p.cin, p.stride, int(up2), c1 > 0, int(pixel_shuffle),
+        key = (n * ho * wo, p.cout, p.kh, p.kw, p.cin, p.stride, int(up2), c1 > 0, d.out_mode,
                res is not None, emb is not None, act, odt)
         tile = _TILE_CACHE.get(key)
         if tile is None:
@@ -171,7 +178,7 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
             tile = _autotune_tile(d, scratch, DMA_TILE_CANDIDATES if dma else TILE_CANDIDATES)
             _TILE_CACHE[key] = tile
 
-    tag = ("conv", flops, (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), int(pixel_shuffle)))
+    tag = ("conv", flops, (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), d.out_mode))
     if splits > 1:
         ws = _splitk_workspace(splits * n * ho * wo * p.cout, x.device)
         _launch(tag, "rdeic_conv2d_splitk", C.byref(d), splits, ws.data_ptr(), ws.numel(), stream_ptr())
@@ -188,6 +195,7 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
 # segments are multiples of 64 run on the LDS-DMA kernel (tile ids 20..34, rdeic_hip.h);
 # the others on the register-staged tiles.
 AUTOTUNE = True
+GEGLU_FUSED = True  # bf16 transformer FF: GEGLU in the projection's epilogue (conv out_mode 2)
 TILE_CANDIDATES = (0, 1, 3, 4, 6, 8, 10)
 DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31)
 _TILE_CACHE: dict = {}
@@ -370,18 +378,20 @@ def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) 
 
 
 def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, out_f32: bool = False) -> torch.Tensor:
-    """Token-wise Linear over a [rows, c] tensor (1x1 conv over a rows x 1 image)."""
+           out: Optional[torch.Tensor] = None, out_f32: bool = False, geglu: bool = False) -> torch.Tensor:
+    """Token-wise Linear over a [rows, c] tensor (1x1 conv over a rows x 1 image).
+    geglu: fused GEGLU projection (p from ParamStore.conv_geglu), output [rows, cout/2]."""
     rows, c = x.shape
     x4 = x.as_strided((1, rows, 1, c), (rows * x.stride(0), x.stride(0), x.stride(0), 1))
     odt = torch.float32 if (out_f32 or x.dtype == torch.float32) else x.dtype
+    cw = p.cout // 2 if geglu else p.cout
     if out is None:
-        out = torch.empty((rows, p.cout), dtype=odt, device=x.device)
-    o4 = out.as_strided((1, rows, 1, p.cout), (rows * out.stride(0), out.stride(0), out.stride(0), 1))
+        out = torch.empty((rows, cw), dtype=odt, device=x.device)
+    o4 = out.as_strided((1, rows, 1, cw), (rows * out.stride(0), out.stride(0), out.stride(0), 1))
     r4 = None
     if res is not None:
         r4 = res.as_strided((1, rows, 1, p.cout), (rows * res.stride(0), res.stride(0), res.stride(0), 1))
-    conv2d(x4, p, act=act, res=r4, out=o4, out_f32=out_f32)
+    conv2d(x4, p, act=act, res=r4, out=o4, out_f32=out_f32, geglu=geglu)
     return out
 
 

@@ -92,6 +92,24 @@ class ParamStore:
             self._packed[key] = p
         return p
 
+    def conv_geglu(self, prefix: str, dtype=None) -> ops.ConvParams:
+        """GEGLU projection (attention.py:49-56, value = rows [0, c), gate = rows [c, 2c)) packed for the
+        fused epilogue (ops.linear(geglu=True)): rows reordered in groups of 4 as (value 4j..4j+3,
+        gate 4j..4j+3), so one 8-wide output chunk holds matching value / gate channels."""
+        dtype = dtype or self.compute_dtype
+        key = (prefix, "geglu", dtype)
+        p = self._packed.get(key)
+        if p is None:
+            w = self.t[prefix + ".weight"]
+            b = self.t.get(prefix + ".bias")
+            c = w.shape[0] // 2
+            if c % 4:
+                raise ValueError("GEGLU width must be a multiple of 4")
+            perm = torch.arange(2 * c, device=w.device).view(2, c // 4, 4).permute(1, 0, 2).reshape(-1)
+            p = ops.ConvParams.pack(w[perm], None if b is None else b[perm], dtype=dtype)
+            self._packed[key] = p
+        return p
+
     def conv_cat(self, prefixes: Sequence[str], dtype=None) -> ops.ConvParams:
         """Several layers with the same input stacked along cout (one GEMM: q|k|v, k|v, emb_layers)."""
         dtype = dtype or self.compute_dtype

@@ -236,8 +236,10 @@ class UNet:
         h = ops.linear(o, s.conv(tb + ".attn2.to_out.0"), res=h)
         # GEGLU feed-forward
         n3 = ops.layer_norm(h, s.get(tb + ".norm3.weight"), s.get(tb + ".norm3.bias"))
-        g = ops.linear(n3, s.conv(tb + ".ff.net.0.proj"))
-        gg = ops.geglu(g)
+        if x.dtype == torch.bfloat16 and ops.GEGLU_FUSED and C % 64 == 0:
+            gg = ops.linear(n3, s.conv_geglu(tb + ".ff.net.0.proj"), geglu=True)  # one pass, half the writes
+        else:
+            gg = ops.geglu(ops.linear(n3, s.conv(tb + ".ff.net.0.proj")))
         h = ops.linear(gg, s.conv(tb + ".ff.net.2"), res=h)
         # proj_out + residual to the block input
         if not x.is_contiguous():

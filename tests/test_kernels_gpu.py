@@ -262,3 +262,29 @@ def test_conv_splitk(gpu, cin, cout, hw, res):
     torch.testing.assert_close(_nchw(out), ref, rtol=2e-2, atol=3e-2)
     out_plain = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
     assert (out.float() - out_plain.float()).abs().max().item() < 0.1
+
+
+@pytest.mark.parametrize("rows,cin,inner", [(4096, 320, 1280), (1000, 640, 2560), (256, 64, 256)])
+def test_linear_fused_geglu(gpu, rows, cin, inner):
+    """GEGLU in the projection's epilogue (conv out_mode 2, weights interleaved by
+    ParamStore.conv_geglu) vs the unfused projection + rdeic_geglu and vs torch fp32."""
+    from rdeic_amd import ops
+    from rdeic_amd.params import ParamStore
+    g = torch.Generator().manual_seed(rows + cin)
+    x = torch.randn(rows, cin, generator=g)
+    w = torch.randn(2 * inner, cin, generator=g) / math.sqrt(cin)
+    b = torch.randn(2 * inner, generator=g) * 0.1
+    st = ParamStore(torch.bfloat16, "cuda")
+    st.shapes["ff.weight"], st.shapes["ff.bias"] = tuple(w.shape), tuple(b.shape)
+    st.t["ff.weight"], st.t["ff.bias"] = w.cuda(), b.cuda()
+    xb = x.to(torch.bfloat16).cuda()
+    fused = ops.linear(xb, st.conv_geglu("ff"), geglu=True)
+    unfused = ops.geglu(ops.linear(xb, st.conv("ff")))
+    assert fused.shape == (rows, inner)
+    assert (fused.float() - unfused.float()).abs().max().item() <= 2e-2 * unfused.float().abs().max().item()
+    h = x.to(torch.bfloat16).float() @ w.to(torch.bfloat16).float().t() + b
+    ref = h[:, :inner] * F.gelu(h[:, inner:])
+    err = (fused.float().cpu() - ref).abs().max().item()
+    assert err <= 3e-2 * ref.abs().max().item(), err
+    with pytest.raises(ValueError):
+        ops.linear(xb, st.conv_geglu("ff"), geglu=True, act=ops.GELU)
