@@ -17,7 +17,7 @@
 #include "../../include/rdeic_hip.h"
 #include "prof.h"
 
-int rdeic_g_attn64 = 1;  // rdeic_set_conv_option(1, v): transposed dh=64 kernel on/off
+int rdeic_g_attn64 = 2;  // rdeic_set_conv_option(1, v): dh=64 kernel: 2 LDS-DMA (default), 1 register-staged, 0 generic
 
 namespace {
 
@@ -422,10 +422,240 @@ __global__ __launch_bounds__(256) void attn64_kernel(const bf16* __restrict__ q,
   }
 }
 
+
+// ============================================================================================
+// bf16, head dim 64, LDS-DMA variant: the math of attn64_kernel (per wave S^T = K Q^T for 32
+// queries, P kept in registers as the PV operand, online softmax in the exp2 domain), with the
+// K and V tiles moved L2 -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging, no ds_write)
+// through a 3-deep ring: counted vmcnt, one raw s_barrier per 64-key tile, two tiles in flight.
+// V stays row-major in LDS; the V^T fragments of O^T += V^T P^T come from ds_read_b64_tr_b16
+// (hardware transpose). Swizzles, applied on the DMA source address: K chunk c of row r at slot
+// c ^ (bit3(r) << 1 | bit1(r) << 2) (conflict-free ds_read_b128 fragment rows, as the conv), V
+// chunk c at slot c ^ (((r >> 1) & 3) << 1) (conflict-free transposed reads). Keys >= lk read
+// zeros through the buffer descriptor's range check and are masked to -inf in the scores.
+// ============================================================================================
+constexpr unsigned kAttnOOB = 0x80000000u;
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_vptr_t;
+
+__device__ __forceinline__ void attn_dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_vptr_t)lds_dst, 16, (int)voff, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16 as inline asm: through the builtin, hipcc treats the read as aliasing the
+// in-flight LDS-DMA and drains vmcnt(0) before it (ending the prefetch). The caller waits
+// lgkmcnt itself before using the result (hipcc does not count asm LDS operations).
+__device__ __forceinline__ v4s ds_read_tr16(unsigned lds_addr) {
+  v4s r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void attn_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int A64D_TILE = 64 * 128, A64D_STAGE = 2 * A64D_TILE, A64D_S = 3;
+
+__global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
+                                                         int ldk, const bf16* __restrict__ v, int ldv,
+                                                         bf16* __restrict__ o, int ldo, int heads, int lq, int lk,
+                                                         float scale_log2, int kv_bcast) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // A64D_S x (K tile | V tile), 128-B rows
+  const int bh = blockIdx.y;
+  const int b = bh / heads, h = bh - b * heads;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, g = lane >> 4;
+  const bf16* qb = q + (long)b * lq * ldq + h * 64;
+  const long kvb = kv_bcast ? 0 : b;
+  const bf16* kb = k + kvb * lk * ldk + h * 64;
+  const bf16* vb = v + kvb * lk * ldv + h * 64;
+  const int qw = blockIdx.x * A64_Q + wave * 32;
+
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int hd = 0; hd < 2; ++hd) {
+      const int qq = qw + 16 * u + lr;
+      bf16x8 z = *reinterpret_cast<const bf16x8*>(qb + (long)min(qq, lq - 1) * ldq + 32 * hd + 8 * g);
+      if (qq >= lq) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
+      }
+      qf[u][hd] = z;
+    }
+
+  const __amdgpu_buffer_rsrc_t rsk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)kb, (short)0, (int)(((long)(lk - 1) * ldk + 64) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)vb, (short)0, (int)(((long)(lk - 1) * ldv + 64) * 2), 0x00020000);
+  // DMA: wave w fills rows 16w .. 16w+15 of the K and V tiles (two 8-row wave-instructions each)
+  const int sl = lane & 7, rsub = lane >> 3;
+  int drow[2];
+  unsigned kco[2], vco[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wave + j) + rsub;
+    drow[j] = row;
+    kco[j] = (unsigned)(sl ^ ((((row >> 3) & 1) << 1) | (((row >> 1) & 1) << 2))) * 16u;
+    vco[j] = (unsigned)(sl ^ (((row >> 1) & 3) << 1)) * 16u;
+  }
+  auto issue = [&](int kt) {
+    char* sb = lds + (kt % A64D_S) * A64D_STAGE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int key = kt * 64 + drow[j];
+      const bool in = key < lk;
+      attn_dma16(rsk, sb + (2 * wave + j) * 1024, in ? (unsigned)key * (unsigned)(ldk * 2) + kco[j] : kAttnOOB);
+      attn_dma16(rsv, sb + A64D_TILE + (2 * wave + j) * 1024,
+                 in ? (unsigned)key * (unsigned)(ldv * 2) + vco[j] : kAttnOOB);
+    }
+  };
+
+  f32x4 oacc[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+
+  // fragment-read addressing (per lane constants)
+  const int krk = ((((lr >> 3) & 1) << 1) | (((lr >> 1) & 1) << 2));  // K row key of rows 16t + lr
+  const int vq = lr >> 2, vp = lr & 3;                                    // tr-read: block row q, column group p
+
+  const int ntiles = (lk + 63) / 64;
+  issue(0);
+  if (ntiles > 1) issue(1);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt + 1 < ntiles) attn_wait_vm<4>(); else attn_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < ntiles) issue(kt + 2);
+    const char* Kt = lds + (kt % A64D_S) * A64D_STAGE;
+    const char* Vt = Kt + A64D_TILE;
+    const int key0 = kt * 64;
+    f32x4 st[2][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const char* kr = Kt + (16 * t + lr) * 128;
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kr + ((g ^ krk) * 16));
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kr + (((4 + g) ^ krk) * 16));
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[u][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[u][1], acc, 0, 0, 0);
+        st[u][t] = acc;
+      }
+    }
+    // V^T fragments for O^T += V^T P^T, read now so the LDS latency hides under the softmax:
+    // lane (lr, g) needs V[keys 32c + 4g + 0..3 (lo) / +16 (hi)][d = 16dt + lr]
+    v4s vt[4][2][2];
+    {
+      const unsigned vbase = (unsigned)(uintptr_t)(lds_vptr_t)Vt;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int hl = 0; hl < 2; ++hl) {
+            const int r = 32 * c + 16 * hl + 4 * g + vq;
+            const int ch = 2 * dt + (vp >> 1);
+            vt[dt][c][hl] = ds_read_tr16(vbase + r * 128 + ((ch ^ (((r >> 1) & 3) << 1)) * 16) + (vp & 1) * 8);
+          }
+    }
+    if (key0 + 64 > lk) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (key0 + 16 * t + 4 * g + i >= lk) st[u][t][i] = -INFINITY;
+    }
+    bf16x8 pf[2][2];
+    bool rescale = false;
+    float alpha[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mx = st[u][0][0];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[u][t][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float ms = mx * scale_log2;
+      alpha[u] = 1.f;
+      if (ms > m_run[u] + 8.f) {
+        alpha[u] = __builtin_amdgcn_exp2f(m_run[u] - ms);
+        m_run[u] = ms;
+        rescale = true;
+      }
+      const float nm = -m_run[u];
+      float ps = 0.f;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[u][2 * c + (j >> 2)][j & 3], scale_log2, nm));
+          ps += p;
+          pf[u][c][j] = (bf16)p;
+        }
+      l_run[u] = l_run[u] * alpha[u] + ps;
+    }
+    if (__any(rescale)) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) oacc[u][dt] *= alpha[u];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm transposed reads above
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const v4s both[2] = {vt[dt][c][0], vt[dt][c][1]};
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(both);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) oacc[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[u][c], oacc[u][dt], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float l = l_run[u];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+    const int qq = qw + 16 * u + lr;
+    if (qq < lq) {
+      bf16* orow = o + ((long)b * lq + qq) * ldo + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 ov;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ov[i] = (bf16)(oacc[u][dt][i] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = ov;
+      }
+    }
+  }
+}
+
 template <typename T>
 int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo, int batch,
                 int heads, int lq, int lk, int dh, float scale, int kv_bcast, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
+    if (dh == 64 && rdeic_g_attn64 == 2 && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 &&
+        (long)(lk - 1) * (ldk > ldv ? ldk : ldv) * 2 + 128 < (1l << 31)) {
+      dim3 grid((lq + A64_Q - 1) / A64_Q, batch * heads);
+      hipLaunchKernelGGL(attn64_dma_kernel, grid, dim3(256), A64D_S * A64D_STAGE, s, (const bf16*)q, ldq,
+                         (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, heads, lq, lk,
+                         scale * 1.4426950408889634f, kv_bcast);
+      return launch_status();
+    }
     if (dh == 64 && rdeic_g_attn64 && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0) {
       dim3 grid((lq + A64_Q - 1) / A64_Q, batch * heads);
       hipLaunchKernelGGL(attn64_kernel, grid, dim3(256), 0, s, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v,

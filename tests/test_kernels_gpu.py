@@ -288,3 +288,30 @@ def test_linear_fused_geglu(gpu, rows, cin, inner):
     assert err <= 3e-2 * ref.abs().max().item(), err
     with pytest.raises(ValueError):
         ops.linear(xb, st.conv_geglu("ff"), geglu=True, act=ops.GELU)
+
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("heads,lq,lk,bcast", [(5, 4096, 4096, False), (10, 300, 77, True), (2, 130, 1000, False)])
+def test_attention_dh64_kernels(gpu, mode, heads, lq, lk, bcast):
+    """The register-staged (1) and LDS-DMA (2) head-dim-64 kernels vs torch fp32 (ragged tiles,
+    broadcast K/V, long keys)."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(lq + lk)
+    B, dh = 2, 64
+    q = torch.randn(B, lq, heads * dh, generator=g)
+    kb = 1 if bcast else B
+    k = torch.randn(kb, lk, heads * dh, generator=g)
+    v = torch.randn(kb, lk, heads * dh, generator=g)
+    qc, kc, vc = (t.to(torch.bfloat16).cuda() for t in (q, k, v))
+    o = torch.empty(B * lq, heads * dh, dtype=torch.bfloat16, device="cuda")
+    prev = ops.set_conv_option(1, mode)
+    try:
+        ops.attention(qc.view(-1, heads * dh), kc.view(-1, heads * dh), vc.view(-1, heads * dh), o, batch=B,
+                      heads=heads, lq=lq, lk=lk, dh=dh, scale=dh ** -0.5, kv_bcast=bcast)
+    finally:
+        ops.set_conv_option(1, prev)
+    qf, kf, vf = (t.to(torch.bfloat16).float() for t in (q, k, v))
+    ref = _ref_attn(qf, kf.expand(B, -1, -1).contiguous(), vf.expand(B, -1, -1).contiguous(), heads, dh, dh ** -0.5)
+    err = (o.float().cpu().view(B, lq, -1) - ref).abs().max().item()
+    assert err < 2e-2, err
