@@ -164,7 +164,8 @@ int rdeic_spaced_step(const float* x, const float* e, const float* noise, int64_
                       float c2, float s, float* xp, float* x0, void* stream);
 /* SiLU in place / copy (fp32), for embedding MLP inputs */
 int rdeic_silu_f32(const float* x, float* y, int64_t count, void* stream);
-/* image u8 HWC <-> model tensors (inference.py:51-52, 85-87) */
+/* image u8 HWC <-> model tensors (inference.py:51-52, 85-87). u8 -> NHWC writes x*2-1 into channels
+ * 0..2 and, when ld <= 16, zeros into channels 3..ld-1 (a zero-padded conv input). */
 int rdeic_image_u8_to_nhwc(const uint8_t* img, int32_t n, int32_t h, int32_t w, void* out, int32_t ld,
                            int32_t dtype, void* stream);
 int rdeic_nhwc_to_image_u8(const void* x, int32_t n, int32_t h, int32_t w, int32_t ld, uint8_t* img,

@@ -139,17 +139,31 @@ class Compression:
             x = self._block(b, x)
         return x
 
+    def _pad_width(self, c: int):
+        """bf16: zero-pad the odd hidden widths of the entropy nets (5/3 and 4/3 of 2c, 224) to 64-channel
+        blocks (16 below 32) so their convs gather 16-byte vectors / run on the LDS-DMA kernel. Encoder and
+        decoder pad identically (the padded channels are exactly 0), so mu / sigma stay identical
+        between them; the fp32 parity mode keeps the reference widths."""
+        if self.store.compute_dtype != torch.bfloat16:
+            return None
+        return -(-c // 64) * 64 if c > 32 else -(-c // 16) * 16
+
     def _ep(self, name: str, i: int, x: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
         s, p = self.store, self.p
-        h = ops.conv2d(x, s.conv(f"{p}{name}.{i}.fusion.0"), x2=x2, act=ops.GELU)
-        h = ops.conv2d(h, s.conv(f"{p}{name}.{i}.fusion.2"), act=ops.GELU)
-        return ops.conv2d(h, s.conv(f"{p}{name}.{i}.fusion.4"))
+        f0, f2, f4 = (f"{p}{name}.{i}.fusion.{j}" for j in (0, 2, 4))
+        w0, w2 = s.shapes[f0 + ".weight"][0], s.shapes[f2 + ".weight"][0]
+        p0, p2 = self._pad_width(w0), self._pad_width(w2)
+        h = ops.conv2d(x, s.conv(f0, cout_pad=p0), x2=x2, act=ops.GELU)
+        h = ops.conv2d(h, s.conv(f2, cin_pad=p0, cout_pad=p2), act=ops.GELU)
+        return ops.conv2d(h, s.conv(f4, cin_pad=p2))
 
     def _channel_ctx(self, i: int, yhat_prefix: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         s, p = self.store, self.p
-        h = ops.conv2d(yhat_prefix, s.conv(f"{p}channel_context.{i}.fushion.0"), act=ops.GELU)
-        h = ops.conv2d(h, s.conv(f"{p}channel_context.{i}.fushion.2"), act=ops.GELU)
-        return ops.conv2d(h, s.conv(f"{p}channel_context.{i}.fushion.4"), out=out)
+        f0, f2, f4 = (f"{p}channel_context.{i}.fushion.{j}" for j in (0, 2, 4))
+        p0 = self._pad_width(s.shapes[f0 + ".weight"][0])
+        h = ops.conv2d(yhat_prefix, s.conv(f0, cout_pad=p0), act=ops.GELU)
+        h = ops.conv2d(h, s.conv(f2, cin_pad=p0), act=ops.GELU)
+        return ops.conv2d(h, s.conv(f4), out=out)
 
     # ------------------------------------------------------------------ VQ
     def _codebook(self) -> torch.Tensor:

@@ -103,14 +103,18 @@ __global__ void silu_f32_kernel(const float* __restrict__ x, float* __restrict__
     y[i] = x[i] / (1.0f + expf(-x[i]));
 }
 
-// img u8 [n][h][w][3] -> x = (u8/255.0 (fp64, then fp32)) * 2 - 1 written NHWC (ld >= 3)
+// img u8 [n][h][w][3] -> x = (u8/255.0 (fp64, then fp32)) * 2 - 1 written NHWC; channels 3 .. cw-1
+// of each pixel are zero-filled (cw = ld when ld <= 16: a zero-padded input for 16-byte gathers)
 template <typename T>
-__global__ void img_to_nhwc_kernel(const uint8_t* __restrict__ img, long pix, T* __restrict__ out, int ld) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pix * 3; i += (long)gridDim.x * blockDim.x) {
-    long p = i / 3;
-    int ch = (int)(i - p * 3);
-    float v = (float)((double)img[i] / 255.0);
-    v = __fsub_rn(__fmul_rn(v, 2.0f), 1.0f);
+__global__ void img_to_nhwc_kernel(const uint8_t* __restrict__ img, long pix, T* __restrict__ out, int ld, int cw) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < pix * cw; i += (long)gridDim.x * blockDim.x) {
+    long p = i / cw;
+    int ch = (int)(i - p * cw);
+    float v = 0.f;
+    if (ch < 3) {
+      v = (float)((double)img[p * 3 + ch] / 255.0);
+      v = __fsub_rn(__fmul_rn(v, 2.0f), 1.0f);
+    }
     out[p * ld + ch] = from_f32<T>(v);
   }
 }
@@ -259,10 +263,12 @@ extern "C" int rdeic_image_u8_to_nhwc(const uint8_t* img, int32_t n, int32_t h, 
   if (!img || !out || n <= 0 || h <= 0 || w <= 0 || ld < 3) return RDEIC_EINVAL;
   long pix = (long)n * h * w;
   hipStream_t s = (hipStream_t)stream;
+  const int cw = ld <= 16 ? ld : 3;
   if (dtype == 1)
-    hipLaunchKernelGGL(img_to_nhwc_kernel<bf16>, dim3(grid_for(pix * 3)), dim3(256), 0, s, img, pix, (bf16*)out, ld);
+    hipLaunchKernelGGL(img_to_nhwc_kernel<bf16>, dim3(grid_for(pix * cw)), dim3(256), 0, s, img, pix, (bf16*)out, ld, cw);
   else
-    hipLaunchKernelGGL(img_to_nhwc_kernel<float>, dim3(grid_for(pix * 3)), dim3(256), 0, s, img, pix, (float*)out, ld);
+    hipLaunchKernelGGL(img_to_nhwc_kernel<float>, dim3(grid_for(pix * cw)), dim3(256), 0, s, img, pix, (float*)out, ld,
+                       cw);
   return launch_status();
 }
 

@@ -366,8 +366,12 @@ def set_conv_option(key: int, value: int) -> int:
 
 
 def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) -> bool:
-    """Same rule as rdeic_conv2d's dispatch to the big-tile path (bf16, 16-byte gathers, cout > 32)."""
-    if CONV_PATH == 0 or x.dtype != torch.bfloat16 or p.cout <= 32:
+    """Same rule as rdeic_conv2d's dispatch to the big-tile path (bf16, 16-byte gathers, cout > 32), plus
+    the large tiny-cout convs (the VAE's conv_out): their direct kernel would redo the GroupNorm + SiLU
+    of every input element for all 9 taps."""
+    if CONV_PATH == 0 or x.dtype != torch.bfloat16:
+        return False
+    if p.cout <= 32 and not (p.cout <= 4 and x.shape[0] * x.shape[1] * x.shape[2] >= (1 << 20)):
         return False
     for t in (x, x2):
         if t is None:

@@ -78,15 +78,24 @@ class ParamStore:
 
     # ------------------------------------------------------------ packed weights
     def conv(self, prefix: str, stride: int = 1, pad: Optional[int] = None, dtype=None,
-             scale: float = 1.0) -> ops.ConvParams:
+             scale: float = 1.0, cin_pad: Optional[int] = None, cout_pad: Optional[int] = None) -> ops.ConvParams:
+        """Packed conv / linear weights. cin_pad / cout_pad zero-extend the input / output channels
+        (zero weight columns / rows and bias): a zero-padded activation keeps 16-byte gathers and
+        64-channel blocks; the padded output channels are exactly act(0) = 0 for GELU / leaky / none."""
         dtype = dtype or self.compute_dtype
-        key = (prefix, stride, pad, dtype, scale)
+        key = (prefix, stride, pad, dtype, scale, cin_pad, cout_pad)
         p = self._packed.get(key)
         if p is None:
             w = self.t[prefix + ".weight"]
             b = self.t.get(prefix + ".bias")
             if scale != 1.0:
                 w, b = w * scale, (None if b is None else b * scale)
+            if cin_pad is not None and cin_pad > w.shape[1]:
+                w = torch.nn.functional.pad(w, (0, 0) * (w.dim() - 2) + (0, cin_pad - w.shape[1]))
+            if cout_pad is not None and cout_pad > w.shape[0]:
+                w = torch.nn.functional.pad(w, (0, 0) * (w.dim() - 1) + (0, cout_pad - w.shape[0]))
+                if b is not None:
+                    b = torch.nn.functional.pad(b, (0, cout_pad - b.shape[0]))
             k = w.shape[-1] if w.dim() == 4 else 1
             p = ops.ConvParams.pack(w, b, stride=stride, pad=(k // 2 if pad is None else pad), dtype=dtype)
             self._packed[key] = p

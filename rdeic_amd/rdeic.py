@@ -112,9 +112,11 @@ class RDEIC:
     def encode_images_nhwc(self, img_u8: torch.Tensor) -> torch.Tensor:
         """uint8 [B,H,W,3] (device) -> h = 0.18215 * Encoder.forward_hc(x*2-1), NHWC compute dtype."""
         B, H, W_, _ = img_u8.shape
-        x = torch.empty((B, H, W_, 3), dtype=self.compute_dtype, device=img_u8.device)
-        ops.call("rdeic_image_u8_to_nhwc", img_u8.contiguous().data_ptr(), B, H, W_, x.data_ptr(), 3, ops.dt_code(x),
-                 ops.stream_ptr())
+        # bf16: 8 channels (3 + 5 zeros) so the VAE's conv_in gathers 16-byte vectors (cin-padded weights)
+        cpad = 8 if self.compute_dtype == torch.bfloat16 else 3
+        x = torch.empty((B, H, W_, cpad), dtype=self.compute_dtype, device=img_u8.device)
+        ops.call("rdeic_image_u8_to_nhwc", img_u8.contiguous().data_ptr(), B, H, W_, x.data_ptr(), cpad,
+                 ops.dt_code(x), ops.stream_ptr())
         return self.first_stage_model.encode_hc(x, out_mul=self.scale_factor)
 
     def encode_nchw_nhwc(self, x: torch.Tensor) -> torch.Tensor:

@@ -119,7 +119,7 @@ class AutoencoderKL:
         """x: NHWC compute-dtype image in [-1, 1] ([B,H,W,3]); returns c * out_mul, [B,H/8,W/8,512]."""
         s = self.store
         e = self.prefix + "encoder."
-        h = ops.conv2d(x, s.conv(e + "conv_in"))
+        h = ops.conv2d(x, s.conv(e + "conv_in", cin_pad=x.shape[3] if x.shape[3] > 3 else None))
         for lvl, down in self.enc_blocks:
             for blk in lvl:
                 h = self.resnet(blk, h)
