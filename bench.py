@@ -168,12 +168,13 @@ def main():
             cpu = run_cpu_baseline(size=S, steps=args.ddim_steps, rate_gain=rate_gain)
         except Exception as e:  # the baseline is reported, never the target
             cpu = {"value": None, "error": f"{type(e).__name__}: {e}"}
+    cfg_name = {(512, 2): "config 2", (1024, 5): "config 3"}.get((S, args.ddim_steps), "custom")
     line = {
-        "metric": "512x512 images/sec encode+relay-decode @ fixed bpp (bitstream-parity path); 1/2/4/8 GPU",
+        "metric": f"{S}x{S} images/sec encode+relay-decode @ fixed bpp (bitstream-parity path); 1/2/4/8 GPU",
         "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded images, random-init weights)",
-        "config": {"workload": f"config 2: batch {B}/GPU {S}x{S}, {args.ddim_steps}-step relay "
+        "config": {"workload": f"{cfg_name}: batch {B}/GPU {S}x{S}, {args.ddim_steps}-step relay "
                                f"{'DDIM' if args.sampler == 'ddim' else 'spaced DDPM'}, "
                                f"encode+entropy-code+decode+VAE-decode", "global_batch": B * world,
                    "image_size": S, "ddim_steps": args.ddim_steps, "sampler": args.sampler, "parallelism": f"dp{world}", "rate_gain": rate_gain,
