@@ -156,6 +156,10 @@ int rdeic_timestep_embedding(const int64_t* t, const float* freqs, int32_t n, in
 /* relay-DDIM eta=0 update (ddim_sampler_relay.py:215-229) with host-precomputed fp32 scalars */
 int rdeic_ddim_step(const float* x, const float* e, int64_t count, float c_sq1m, float c_sqa, float c_sqap,
                     float c_dir, float* xp, float* x0, void* stream);
+/* classifier-free guidance combine out = e_uncond + scale * (e_cond - e_uncond), fp32, the reference's op
+ * order (ddim_sampler_relay.py:188-192 p_sample_ddim; spaced_sampler_relay.py:277-283 predict_noise) */
+int rdeic_cfg_combine(const float* e_cond, const float* e_uncond, int64_t count, float scale, float* out,
+                      void* stream);
 /* relay spaced (DDPM) update (spaced_sampler_relay.py:270-275 _predict_xstart_from_eps, :154-170
  * q_posterior_mean_variance, :378-383 x_prev): pred_x0 = a*x - b*e, mean = c1*pred_x0 + c2*x,
  * xp = mean + s*noise (s = nonzero_mask * sqrt(model_variance)); fp32 scalars from the host's

@@ -79,6 +79,7 @@ PROTOTYPES = {
     "rdeic_timestep_embedding": (C.c_int, [_p, _p, _i32, _i32, _p, _p]),
     "rdeic_ddim_step": (C.c_int, [_p, _p, _i64, _f, _f, _f, _f, _p, _p, _p]),
     "rdeic_spaced_step": (C.c_int, [_p, _p, _p, _i64, _f, _f, _f, _f, _f, _p, _p, _p]),
+    "rdeic_cfg_combine": (C.c_int, [_p, _p, _i64, _f, _p, _p]),
     "rdeic_silu_f32": (C.c_int, [_p, _p, _i64, _p]),
     "rdeic_image_u8_to_nhwc": (C.c_int, [_p, _i32, _i32, _i32, _p, _i32, _i32, _p]),
     "rdeic_nhwc_to_image_u8": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _p]),

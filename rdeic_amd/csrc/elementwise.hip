@@ -74,6 +74,16 @@ __global__ void ddim_step_kernel(const float* __restrict__ x, const float* __res
   }
 }
 
+// Classifier-free guidance, the reference's op order (ddim_sampler_relay.py:188-192,
+// spaced_sampler_relay.py:277-283): e = e_u + s * (e_c - e_u), each op rounded on its own.
+__global__ void cfg_combine_kernel(const float* __restrict__ ec, const float* __restrict__ eu, long count, float s,
+                                   float* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < count; i += (long)gridDim.x * blockDim.x) {
+    const float u = eu[i];
+    out[i] = __fadd_rn(u, __fmul_rn(s, __fsub_rn(ec[i], u)));
+  }
+}
+
 // Spaced (DDPM) update in the reference's op order, every product and sum rounded on its own:
 //   pred_x0 = A * x - B * e;   mean = C1 * pred_x0 + C2 * x;   x' = mean + S * noise
 __global__ void spaced_step_kernel(const float* __restrict__ x, const float* __restrict__ e,
@@ -232,6 +242,14 @@ extern "C" int rdeic_ddim_step(const float* x, const float* e, int64_t count, fl
   if (!x || !e || !xp || count <= 0) return RDEIC_EINVAL;
   hipLaunchKernelGGL(ddim_step_kernel, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream, x, e, (long)count,
                      c_sq1m, c_sqa, c_sqap, c_dir, xp, x0);
+  return launch_status();
+}
+
+extern "C" int rdeic_cfg_combine(const float* e_cond, const float* e_uncond, int64_t count, float scale, float* out,
+                                 void* stream) {
+  if (!e_cond || !e_uncond || !out || count <= 0) return RDEIC_EINVAL;
+  hipLaunchKernelGGL(cfg_combine_kernel, dim3(grid_for(count)), dim3(256), 0, (hipStream_t)stream, e_cond, e_uncond,
+                     (long)count, scale, out);
   return launch_status();
 }
 

@@ -55,9 +55,14 @@ class DDIMSampler:
 
     @torch.no_grad()
     def sample_nhwc(self, S: int, x_T: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor,
-                    eta: float = 0.0, ts_tensors=None) -> torch.Tensor:
+                    eta: float = 0.0, ts_tensors=None, unconditional_guidance_scale: float = 1.0,
+                    uc_hint: torch.Tensor = None, uc_context: torch.Tensor = None) -> torch.Tensor:
         """Internal path: x_T fp32 NHWC, guide_hint NHWC (compute dtype). Returns samples fp32 NHWC.
-        ts_tensors: optional {timestep: int64 [B] device tensor} prepared outside a recorded plan."""
+        ts_tensors: optional {timestep: int64 [B] device tensor} prepared outside a recorded plan.
+        Guidance (p_sample_ddim :186-192): with an unconditional (uc_hint, uc_context) and a scale
+        != 1, e = e_u + scale * (e_c - e_u) where e_u is the FULL relay model (control included)
+        evaluated on the unconditional hint and context."""
+        guided = (uc_hint is not None or uc_context is not None) and unconditional_guidance_scale != 1.0
         self.make_schedule(S, ddim_eta=eta)
         if eta != 0.0:
             raise NotImplementedError("relay decoding uses eta = 0 (inference.py:78)")
@@ -70,6 +75,9 @@ class DDIMSampler:
             ts = (ts_tensors[int(step)] if ts_tensors is not None else
                   torch.full((B,), int(step), dtype=torch.long, device=x.device))
             e = self.model.eps_nhwc(x, ts, guide_hint, context)
+            if guided:
+                e_u = self.model.eps_nhwc(x, ts, uc_hint, uc_context)
+                e = ops.cfg_combine(e, e_u, unconditional_guidance_scale)
             c_sq1m, c_sqa, c_sqap, c_dir, _ = self._step_scalars(index)
             xp = torch.empty_like(x)
             ops.call("rdeic_ddim_step", x.data_ptr(), e.data_ptr(), x.numel(), c_sq1m, c_sqa, c_sqap, c_dir,
@@ -81,8 +89,6 @@ class DDIMSampler:
     def sample(self, S, batch_size, shape, conditioning=None, callback=None, eta=0.0, x_T=None, verbose=True,
                unconditional_guidance_scale=1.0, unconditional_conditioning=None, **kwargs):
         """Reference signature (ddim_sampler_relay.py:54-120); NCHW in / out."""
-        if unconditional_conditioning is not None and unconditional_guidance_scale != 1.0:
-            raise NotImplementedError("classifier-free guidance is not on the relay-decode hot path")
         C, H, W_ = shape
         dev = self.model.device
         if x_T is None:
@@ -90,6 +96,12 @@ class DDIMSampler:
         x = ops.nchw_to_nhwc(x_T.float().to(dev), torch.float32)
         hint = ops.nchw_to_nhwc(conditioning["guide_hint"].float().to(dev), self.model.compute_dtype)
         ctx = torch.cat(conditioning["c_crossattn"], 1)
-        samples = self.sample_nhwc(S, x, hint, ctx, eta=eta)
+        uc_hint = uc_ctx = None
+        if unconditional_conditioning is not None and unconditional_guidance_scale != 1.0:
+            uc = unconditional_conditioning
+            uc_hint = ops.nchw_to_nhwc(uc["guide_hint"].float().to(dev), self.model.compute_dtype)
+            uc_ctx = torch.cat(uc["c_crossattn"], 1)
+        samples = self.sample_nhwc(S, x, hint, ctx, eta=eta, unconditional_guidance_scale=unconditional_guidance_scale,
+                                   uc_hint=uc_hint, uc_context=uc_ctx)
         out = ops.nhwc_to_nchw(samples)
         return out, {"x_inter": [x_T, out], "pred_x0": [x_T]}

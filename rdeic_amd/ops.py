@@ -500,6 +500,16 @@ def geglu(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     return out
 
 
+def cfg_combine(e_cond: torch.Tensor, e_uncond: torch.Tensor, scale: float) -> torch.Tensor:
+    """Classifier-free guidance e_u + scale * (e_c - e_u) (fp32, the reference's op order)."""
+    if e_cond.dtype != torch.float32 or e_uncond.dtype != torch.float32 or e_cond.shape != e_uncond.shape:
+        raise ValueError("cfg_combine needs two fp32 tensors of one shape")
+    ec, eu = e_cond.contiguous(), e_uncond.contiguous()
+    out = torch.empty_like(ec)
+    call("rdeic_cfg_combine", ec.data_ptr(), eu.data_ptr(), ec.numel(), float(scale), out.data_ptr(), stream_ptr())
+    return out
+
+
 def nchw_to_nhwc(x: torch.Tensor, dtype, mul: float = 1.0, add: float = 0.0, out=None) -> torch.Tensor:
     x = x.to(torch.float32).contiguous()
     n, c, h, w = x.shape

@@ -137,6 +137,10 @@ class RDEIC:
     def eps_nhwc(self, x: torch.Tensor, t: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor):
         return self.control_model.forward(x, guide_hint, t, context.to(self.device))
 
+    def eps_uncond_nhwc(self, x: torch.Tensor, t: torch.Tensor, context: torch.Tensor):
+        """Base UNet alone, no control branch (NoiseEstimator.forward_unconditional, rdeic.py:214-235)."""
+        return self.control_model.forward_unconditional(x, t, context.to(self.device))
+
     def decode_nhwc(self, z: torch.Tensor, out_f32: bool = True, consts=None) -> torch.Tensor:
         """z: fp32 NHWC latent sample -> decoder output NHWC [B,8h,8w,3] (1/scale_factor fused)."""
         B = z.shape[0]
@@ -191,6 +195,13 @@ class RDEIC:
         hint_nhwc = ops.nchw_to_nhwc(hint.float().to(self.device), self.compute_dtype)
         eps = self.eps_nhwc(x, t.to(self.device), hint_nhwc, ctx)
         return ops.nhwc_to_nchw(eps)
+
+    @torch.no_grad()
+    def apply_model_unconditional(self, x_noisy: torch.Tensor, t: torch.Tensor, cond: dict) -> torch.Tensor:
+        """rdeic.py:700-709: the base UNet with cond's text context, no control features."""
+        ctx = torch.cat(cond["c_crossattn"], 1)
+        x = ops.nchw_to_nhwc(x_noisy.float().to(self.device), torch.float32)
+        return ops.nhwc_to_nchw(self.eps_uncond_nhwc(x, t.to(self.device), ctx))
 
     @torch.no_grad()
     def decode_first_stage(self, z: torch.Tensor) -> torch.Tensor:

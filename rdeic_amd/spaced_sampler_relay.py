@@ -119,10 +119,15 @@ class SpacedSampler:
 
     @torch.no_grad()
     def sample_nhwc(self, steps: int, x_T: torch.Tensor, guide_hint: torch.Tensor, context: torch.Tensor,
-                    step_noise: Optional[Sequence[torch.Tensor]] = None, ts_tensors=None) -> torch.Tensor:
+                    step_noise: Optional[Sequence[torch.Tensor]] = None, ts_tensors=None,
+                    unconditional_guidance_scale: float = 1.0, guided: bool = False) -> torch.Tensor:
         """Internal path: x_T fp32 NHWC, guide_hint NHWC (compute dtype); step_noise[i] (fp32, x's
         layout) is the noise the i-th step draws (steps taken from high t to low). Returns fp32 NHWC.
-        ts_tensors: optional {timestep: int64 [B] device tensor} prepared outside a recorded plan."""
+        ts_tensors: optional {timestep: int64 [B] device tensor} prepared outside a recorded plan.
+        Guidance (predict_noise :277-283): when `guided` (an unconditional conditioning was given or
+        the scale != 1), e = e_u + scale * (e_c - e_u) with e_u from the base UNet alone on the SAME
+        text context (apply_model_unconditional, no control) — unlike the DDIM sampler."""
+        guided = guided or unconditional_guidance_scale != 1.0
         self.make_schedule(steps)
         x = x_T.contiguous()
         B = x.shape[0]
@@ -135,6 +140,8 @@ class SpacedSampler:
             ts = (ts_tensors[int(step)] if ts_tensors is not None else
                   torch.full((B,), int(step), dtype=torch.long, device=x.device))
             e = self.model.eps_nhwc(x, ts, guide_hint, context)
+            if guided:
+                e = ops.cfg_combine(e, self.model.eps_uncond_nhwc(x, ts, context), unconditional_guidance_scale)
             a, b, c1, c2, s = self.step_scalars(index)
             nz = step_noise[i] if step_noise is not None else torch.randn_like(x)
             if tuple(nz.shape) != tuple(x.shape) or nz.dtype != torch.float32 or not nz.is_contiguous():
@@ -152,8 +159,6 @@ class SpacedSampler:
         NCHW fp32 tensor per step (the reference's per-step randn_like), or None."""
         if cond_fn is not None:
             raise NotImplementedError("classifier guidance (cond_fn) is not on the relay-decode hot path")
-        if unconditional_conditioning is not None or unconditional_guidance_scale != 1.0:
-            raise NotImplementedError("classifier-free guidance is not on the relay-decode hot path")
         dev = self.model.device
         if x_T is None:
             x_T = torch.randn(shape, device=dev)
@@ -163,4 +168,6 @@ class SpacedSampler:
         nz = None
         if step_noise is not None:
             nz = [ops.nchw_to_nhwc(n.float().to(dev), torch.float32) for n in step_noise]
-        return ops.nhwc_to_nchw(self.sample_nhwc(steps, x, hint, ctx, step_noise=nz))
+        return ops.nhwc_to_nchw(self.sample_nhwc(steps, x, hint, ctx, step_noise=nz,
+                                                 unconditional_guidance_scale=unconditional_guidance_scale,
+                                                 guided=unconditional_conditioning is not None))

@@ -310,6 +310,29 @@ class NoiseEstimator:
         with ops.splitk_allowed():
             return self._forward(x, hint, t, ctx)
 
+    def forward_unconditional(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
+        """NoiseEstimator.forward_unconditional (rdeic.py:214-235): the base UNet alone, with its own
+        time MLP; no control branch and no zero convs. Used by the spaced sampler's CFG."""
+        with ops.splitk_allowed():
+            s = self.store
+            dt = s.compute_dtype
+            t = t.to(device=x.device, dtype=torch.int64).contiguous()
+            emb_b = self.base.time_embed(self.timestep_embedding(t))
+            ctx = ctx.to(dt).contiguous()
+            Bc, Lc, Dc = ctx.shape
+            ctx_rows = ctx.view(Bc * Lc, Dc)
+            h_base = ops.cast(x, dt)
+            hs_base = []
+            for lb in self.base.input_blocks:
+                h_base = self.base.run_layers(lb, h_base, emb_b, ctx_rows, Bc, Lc)
+                hs_base.append(h_base)
+            h_base = self.base.run_layers(self.base.middle, h_base, emb_b, ctx_rows, Bc, Lc)
+            for lb in self.base.output_blocks:
+                h_base = self.base.run_layers(lb, h_base, emb_b, ctx_rows, Bc, Lc, x2=hs_base.pop())
+            p = self.base.prefix
+            ab = ops.group_norm_ab(h_base, s.get(p + "out.0.weight"), s.get(p + "out.0.bias"), 32, 1e-5)
+            return ops.conv2d(h_base, s.conv(p + "out.2"), gn=ab, gn_silu=True, out_f32=True)
+
     def _forward(self, x: torch.Tensor, hint: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
         """x: fp32 NHWC [B,h,w,4] latent; hint: NHWC [B,h,w,256] (compute dtype);
         t: int64 [B]; ctx: [Bc,77,1024] (compute dtype, Bc in {1, B}). Returns eps fp32 NHWC."""
