@@ -419,6 +419,8 @@ class Compression:
         self.update()
         B = len(strings_list)
         hz, wz = int(shape[0]), int(shape[1])
+        if not (0 < hz <= 1024 and 0 < wz <= 1024 and hz * wz <= 65536):  # a 16384^2 image has a 256^2 z
+            raise ValueError(f"implausible hyper-latent shape {(hz, wz)} (corrupted header?)")
         zi = np.stack([coders.ac_decode_uniform(st[1][0], hz * wz, self.codebook_size) for st in strings_list])
         z_idx = torch.from_numpy(zi.astype(np.int32).reshape(B, hz, wz)).to(device)
 
