@@ -211,6 +211,37 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restri
   for (int j = lane; j < cols; j += 64) pr[j] = from_f32<T>(__expf(sr[j] * scale - mx) * inv);
 }
 
+// Register-resident variant for cols = 64 * NPL: one HBM read of the fp32 scores instead of three.
+// Lane l still owns columns l + 64 k and sums them in the same order, so the result is bit-identical
+// to softmax_rows_kernel (each load is one coalesced 256-byte wave access).
+template <typename T, int NPL>
+__global__ __launch_bounds__(256) void softmax_rows_reg_kernel(const float* __restrict__ s, long rows, float scale,
+                                                               T* __restrict__ p) {
+  constexpr int cols = 64 * NPL;
+  long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* sr = s + row * cols;
+  float v[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) v[k] = __builtin_nontemporal_load(sr + lane + 64 * k) * scale;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) mx = fmaxf(mx, v[k]);
+  mx = warp_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    v[k] = __expf(v[k] - mx);
+    sum += v[k];
+  }
+  sum = warp_sum(sum);
+  float inv = 1.f / sum;
+  T* pr = p + row * cols;
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) pr[lane + 64 * k] = from_f32<T>(v[k] * inv);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ in, int rows, int cols, int ldin,
                                                         T* __restrict__ out, int ldout, long in_bs, long out_bs) {
@@ -700,6 +731,20 @@ extern "C" int rdeic_softmax_rows(const float* s, int64_t rows, int32_t cols, fl
   if (!s || !p || rows <= 0 || cols <= 0) return RDEIC_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4));
+#define RDEIC_SOFTMAX_REG(NPL)                                                                                  \
+  if (cols == 64 * NPL) {                                                                                        \
+    if (dtype == 1)                                                                                              \
+      hipLaunchKernelGGL((softmax_rows_reg_kernel<bf16, NPL>), grid, dim3(256), 0, st, s, (long)rows, scale,     \
+                         (bf16*)p);                                                                              \
+    else                                                                                                         \
+      hipLaunchKernelGGL((softmax_rows_reg_kernel<float, NPL>), grid, dim3(256), 0, st, s, (long)rows, scale,    \
+                         (float*)p);                                                                             \
+    return launch_status();                                                                                      \
+  }
+  RDEIC_SOFTMAX_REG(16)
+  RDEIC_SOFTMAX_REG(32)
+  RDEIC_SOFTMAX_REG(64)
+#undef RDEIC_SOFTMAX_REG
   if (dtype == 1)
     hipLaunchKernelGGL(softmax_rows_kernel<bf16>, grid, dim3(256), 0, st, s, (long)rows, cols, scale, (bf16*)p);
   else

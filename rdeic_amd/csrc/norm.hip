@@ -224,7 +224,11 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
 }
 
 // 16-byte vectorised variant: one thread = 8 bf16 channels of one pixel (c, ld, yld multiples of 8);
-// grid (x, image), 32-bit indexing inside an image, 4 chunks per thread for loads in flight.
+// grid (x, image), 32-bit indexing inside an image, U chunks per thread for loads in flight. When
+// 256 % (c / 8) == 0 (every VAE / compressor width: 128, 256, 512) a thread's U chunks share one
+// channel group, so its 64 bytes of (a, b) are loaded once instead of U times (the per-chunk table
+// reads were 4x the x traffic through L1 / TA).
+template <bool UNIFORM, int U>
 __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const bf16* __restrict__ x, int n, int hw, int c, int ld,
                                                            const float* __restrict__ ab, int ab_c, int silu,
                                                            float out_mul, bf16* __restrict__ y, int yld) {
@@ -234,24 +238,30 @@ __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const bf16* __restric
   const bf16* xi = x + (long)img * hw * ld;
   bf16* yi = y + (long)img * hw * yld;
   const float* abi = ab + (long)img * ab_c * 2;
-  const int base = blockIdx.x * 1024 + threadIdx.x;
-  bf16x8 v[4];
-  int pix[4], ch[4];
+  const int base = blockIdx.x * (256 * U) + threadIdx.x;
+  bf16x8 v[U];
+  int pix[U], ch[U];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int i = base + u * 256;
     pix[u] = i / cp;
     ch[u] = (i - pix[u] * cp) * 8;
     if (i < total) v[u] = *reinterpret_cast<const bf16x8*>(xi + (long)pix[u] * ld + ch[u]);
   }
+  float4 sab[4];
+  if (UNIFORM) {
+    const float4* p = reinterpret_cast<const float4*>(abi + ch[0] * 2);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+    for (int q = 0; q < 4; ++q) sab[q] = p[q];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
     if (base + u * 256 >= total) break;
     const float4* p = reinterpret_cast<const float4*>(abi + ch[u] * 2);
     bf16x8 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float4 s = p[q];  // (a, b) of channels ch+2q, ch+2q+1
+      float4 s = UNIFORM ? sab[q] : p[q];  // (a, b) of channels ch+2q, ch+2q+1
       float v0 = (float)v[u][2 * q] * s.x + s.y;
       float v1 = (float)v[u][2 * q + 1] * s.z + s.w;
       if (silu) {  // x * rcp(1 + e^-x): v_rcp instead of the IEEE divide sequence (bf16 output)
@@ -399,9 +409,15 @@ extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32
   if (dtype == 1 && c % 8 == 0 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
       ((uintptr_t)y) % 16 == 0 && ((uintptr_t)ab) % 16 == 0) {
     if ((long)hw * (c / 8) >= (1L << 31) - 2048) return RDEIC_EINVAL;
-    const int blocks = (int)(((long)hw * (c / 8) + 1023) / 1024);
-    hipLaunchKernelGGL(gn_apply_vec_kernel, dim3(blocks, n), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld, ab, ab_c,
-                       silu, out_mul, (bf16*)y, yld);
+    if (256 % (c / 8) == 0) {
+      const int blocks = (int)(((long)hw * (c / 8) + 2047) / 2048);
+      hipLaunchKernelGGL((gn_apply_vec_kernel<true, 8>), dim3(blocks, n), dim3(256), 0, s, (const bf16*)x, n, hw, c, ld,
+                         ab, ab_c, silu, out_mul, (bf16*)y, yld);
+    } else {
+      const int blocks = (int)(((long)hw * (c / 8) + 1023) / 1024);
+      hipLaunchKernelGGL((gn_apply_vec_kernel<false, 4>), dim3(blocks, n), dim3(256), 0, s, (const bf16*)x, n, hw, c,
+                         ld, ab, ab_c, silu, out_mul, (bf16*)y, yld);
+    }
     return launch_status();
   }
   int blocks = (int)std::min<long>((total + 255) / 256, 16384);
