@@ -571,12 +571,14 @@ int launch_plain_auto(const ConvArgs& a, hipStream_t s, int tile = -1) {
 // ============================================================================================
 // Tiny-cout direct 3x3 conv (cout <= 4; the VAE decoder's conv_out 128 -> 3 with GroupNorm +
 // SiLU on its input). An MFMA tile would compute 16 columns for 3 useful ones and re-apply GN on
-// every gathered element, so this is a VALU kernel instead: a 256-thread block owns a 16x16
+// every gathered element, so this is a VALU (bf16 dot2) kernel instead: a 256-thread block owns a 16x16
 // output patch; per 32-channel chunk the 18x18 input halo is staged once into LDS (GN affine +
 // SiLU applied there, rounded to bf16 exactly like the materialised GN path), the chunk's
 // weights go to LDS as fp32, and each thread accumulates its pixel's COUT outputs in fp32.
 // HBM traffic ~= one read of the input (+ halo) and one write of the output.
 // ============================================================================================
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
 template <int COUT>
 __global__ __launch_bounds__(256) void conv3x3_smallc_kernel(ConvArgs a) {
   constexpr int CC = 32, PS = 40;  // channels per chunk; LDS pixel stride in bf16 (80 B: bank spread)
@@ -618,11 +620,16 @@ __global__ __launch_bounds__(256) void conv3x3_smallc_kernel(ConvArgs a) {
 #pragma unroll
         for (int o = 0; o < COUT; ++o)
           wv[o] = *reinterpret_cast<const bf16x8*>(wp + (long)o * a.wld + t * cin + c0 + c8);
+        // v_dot2_f32_bf16: two bf16 products summed into the fp32 accumulator per instruction,
+        // no bf16 -> fp32 conversions (they were 4 of every 7 VALU ops of the fmaf form)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = (float)xv[e];
+        for (int e = 0; e < 8; e += 2) {
+          const bf16x2 x2 = {xv[e], xv[e + 1]};
 #pragma unroll
-          for (int o = 0; o < COUT; ++o) acc[o] = fmaf(x, (float)wv[o][e], acc[o]);
+          for (int o = 0; o < COUT; ++o) {
+            const bf16x2 w2 = {wv[o][e], wv[o][e + 1]};
+            acc[o] = __builtin_amdgcn_fdot2_f32_bf16(x2, w2, acc[o], false);
+          }
         }
       }
     }

@@ -26,7 +26,7 @@ def _tol(dtype):
 @pytest.mark.parametrize("cin,cout,k,stride,pad,h", [
     (64, 64, 3, 1, 1, 16), (128, 320, 3, 1, 1, 12), (320, 640, 3, 2, 1, 16), (4, 320, 3, 1, 1, 8),
     (256, 16, 5, 1, 2, 8), (48, 224, 5, 1, 2, 8), (512, 8, 1, 1, 0, 8), (260, 64, 3, 1, 1, 8),
-    (3, 128, 3, 1, 1, 16), (256, 1024, 1, 1, 0, 4)])
+    (3, 128, 3, 1, 1, 16), (256, 1024, 1, 1, 0, 4), (128, 3, 3, 1, 1, 16)])
 def test_conv2d(gpu, dtype, cin, cout, k, stride, pad, h):
     from rdeic_amd import ops
     g = torch.Generator().manual_seed(cin * 1000 + cout)
