@@ -1,0 +1,72 @@
+"""Parity at config 3's size (BASELINE.json configs[2]: 1024x1024 images, latent 128², y 64²,
+z 16², 1,048,576 entropy-coded symbols per image), through the HIP path.
+
+* fp32: the GPU's compressor nets + checkerboard stages + rANS/AC coders, fed the GPU's own VAE
+  feature h, write the same file body as the CPU oracle (oracle/model_ref.compress, which restates
+  model/compression.py:151-213 + utils/ckbd.py:76-134) fed that same h; decompressing that body
+  reproduces the oracle's c_latent / guide_hint (compression.py:215-273) within fp32 tolerance.
+* bf16: size-independent properties — the decoder decodes its own streams, coding is
+  batch-invariant (solo bytes == in-batch bytes, solo latents == in-batch latents), and a 5-step
+  relay decode (config 3's S) of the batch returns finite pixels of the right shape.
+The images are the seeded synthetic generator's; weights are the counter-based
+synthetic set at the bench's rate gain (~0.08 bpp at 512²)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+SIZE = 1024
+
+
+def _imgs(n):
+    from rdeic_amd.synthetic import synth_image
+    return torch.from_numpy(np.stack([synth_image(SIZE, SIZE, 231 + i) for i in range(n)])).cuda()
+
+
+def test_config3_fp32_bitstream_and_decompress_vs_oracle(gpu):
+    from oracle import model_ref as M
+    from rdeic_amd import weights as W
+    from rdeic_amd.rdeic import RDEIC
+    g = W.RATE_GAIN_BPP008
+    m32 = RDEIC(compute_dtype=torch.float32).init_synthetic(rate_gain=g)
+    imgs = _imgs(1)
+    h = m32.encode_images_nhwc(imgs)
+    assert tuple(h.shape) == (1, SIZE // 8, SIZE // 8, 512)
+    out = m32.preprocess_model.compress(h)
+    from rdeic_amd import bitstream
+    body = bitstream.pack_body(out[0]["shape"], out[0]["strings"])
+    sd = M.synthetic_state_dict(rate_gain=g)
+    tables = M.Tables()
+    h_cpu = h.permute(0, 3, 1, 2).contiguous().cpu()
+    with torch.no_grad():
+        ref_body, ref_sym, _ = M.compress(sd, h_cpu, tables, coder="c")
+    assert np.asarray(ref_sym).size == (SIZE // 16) ** 2 * 256  # 1,048,576 symbols
+    print(f"1024² body {len(body)} B ({8.0 * len(body) / SIZE ** 2:.4f} bpp), oracle {len(ref_body)} B")
+    assert body == ref_body
+    c_lat, hint = m32.decompress_bodies([body])
+    with torch.no_grad():
+        c_ref, h_ref = M.decompress(sd, ref_body, tables, coder="c")
+    for got, ref in ((c_lat, c_ref), (hint, h_ref)):
+        got = got.float().permute(0, 3, 1, 2).cpu()
+        err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+        assert err < 1e-4, err
+
+
+def test_config3_bf16_self_consistent_and_batch_invariant(gpu):
+    from rdeic_amd import weights as W
+    from rdeic_amd.rdeic import RDEIC
+    from rdeic_amd.synthetic import synth_context, sampler_noise
+    m16 = RDEIC(compute_dtype=torch.bfloat16).init_synthetic(rate_gain=W.RATE_GAIN_BPP008)
+    imgs = _imgs(2)
+    bodies = m16.compress_images(imgs)
+    solo = m16.compress_images(imgs[1:2])
+    assert solo[0] == bodies[1]
+    c_b, h_b = m16.decompress_bodies(bodies)
+    c_s, h_s = m16.decompress_bodies(bodies[1:])
+    assert torch.equal(c_b[1:2], c_s) and torch.equal(h_b[1:2], h_s)
+    ctx = synth_context().cuda()
+    _, noise = sampler_noise((2, 4, SIZE // 8, SIZE // 8), 231)
+    out, bodies2 = m16.codec_images(imgs, ctx, noise, steps=5)
+    assert bodies2 == bodies
+    assert tuple(out.shape) == (2, SIZE, SIZE, 3) and out.dtype == torch.uint8
+    print("config-3 bpp:", [round(8.0 * len(b) / SIZE ** 2, 4) for b in bodies])
