@@ -199,24 +199,28 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ q, int 
 // the B operand of O^T += V^T P^T. The 32-key contraction of each PV MFMA runs in a permuted key
 // order (k slot 8*lg + j <-> key 32s + 16*(j>>2) + 4*lg + (j&3)); V^T is read in the same order.
 // O^T lands as lane = query, 4 consecutive head-dim values per lane -> one 8-byte store.
-template <int DH>
+template <int DH, int NQ, int KTL>
 __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict__ q, int ldq,
                                                          const bf16* __restrict__ k, int ldk,
                                                          const bf16* __restrict__ v, int ldv, bf16* __restrict__ o,
                                                          int ldo, int heads, int lq, int lk, float scale_log2,
                                                          int kv_bcast) {
+  // NQ groups of 16 queries per wave share every staged K/V tile of KTL keys (fewer barriers and
+  // LDS fills per score); the 2-stage barrier pattern is the generic kernel's.
   static_assert(DH == 16 || DH == 32, "small-head kernel");
-  constexpr int DP = 32;        // QK^T contraction padded to the bf16 MFMA k
-  constexpr int KROW = DP + 8;  // K tile row stride (elements)
-  constexpr int VROW = KT + 8;  // V^T tile row stride
+  constexpr int DP = 32;         // QK^T contraction padded to the bf16 MFMA k
+  constexpr int KROW = DP + 8;   // K tile row stride (elements)
+  constexpr int VROW = KTL + 8;  // V^T tile row stride
   constexpr int NDT = DH / 16;
-  constexpr int CPR = DH / 8;   // 16-byte chunks per K/V row
-  __shared__ __attribute__((aligned(16))) bf16 Ks[KT * KROW];
+  constexpr int CPR = DH / 8;    // 16-byte chunks per K/V row
+  constexpr int NT = KTL / 16;   // S^T sub-tiles per key tile
+  constexpr int NS = KTL / 32;   // PV MFMAs per key tile (per d tile)
+  __shared__ __attribute__((aligned(16))) bf16 Ks[KTL * KROW];
   __shared__ __attribute__((aligned(16))) bf16 Vt[DH * VROW];
 
   const int bh = blockIdx.y;
   const int b = bh / heads, h = bh - b * heads;
-  const int q0 = blockIdx.x * QT;
+  const int q0 = blockIdx.x * (64 * NQ);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const bf16* qb = q + (long)b * lq * ldq + h * DH;
@@ -224,28 +228,35 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
   const bf16* kb = k + kvb * lk * ldk + h * DH;
   const bf16* vb = v + kvb * lk * ldv + h * DH;
 
-  const int myq = q0 + wave * 16 + lr;
-  bf16x8 qf;
+  bf16x8 qf[NQ];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) qf[e] = (bf16)0.f;
-  if (myq < lq && 8 * lg < DH) qf = *reinterpret_cast<const bf16x8*>(qb + (long)myq * ldq + 8 * lg);
-
+  for (int g = 0; g < NQ; ++g) {
+    const int myq = q0 + (wave * NQ + g) * 16 + lr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qf[g][e] = (bf16)0.f;
+    if (myq < lq && 8 * lg < DH) qf[g] = *reinterpret_cast<const bf16x8*>(qb + (long)myq * ldq + 8 * lg);
+  }
   if constexpr (DP > DH) {  // K pad columns: zero once, the staging never writes them
-    for (int idx = tid; idx < KT * (DP - DH); idx += 256) {
+    for (int idx = tid; idx < KTL * (DP - DH); idx += 256) {
       const int kr = idx / (DP - DH), dd = DH + idx % (DP - DH);
       Ks[kr * KROW + dd] = (bf16)0.f;
     }
   }
-  f32x4 oacc[NDT];
+  f32x4 oacc[NQ][NDT];
+  float m_run[NQ], l_part[NQ];
 #pragma unroll
-  for (int u = 0; u < NDT; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_part = 0.f;
+  for (int g = 0; g < NQ; ++g) {
+    m_run[g] = -INFINITY;
+    l_part[g] = 0.f;
+#pragma unroll
+    for (int u = 0; u < NDT; ++u) oacc[g][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
-  const int ntiles = (lk + KT - 1) / KT;
+  const int ntiles = (lk + KTL - 1) / KTL;
   for (int kt = 0; kt < ntiles; ++kt) {
-    const int key0 = kt * KT;
+    const int key0 = kt * KTL;
     __syncthreads();
-    for (int cidx = tid; cidx < KT * CPR; cidx += 256) {
+    for (int cidx = tid; cidx < KTL * CPR; cidx += 256) {
       const int kr = cidx / CPR, ch = cidx - kr * CPR;
       const int key = key0 + kr;
       bf16x8 kv, vv;
@@ -261,66 +272,79 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
     }
     __syncthreads();
 
-    // S^T tile t: lane holds S^T[key 16t + 4lg + i][query lr]
-    f32x4 sacc[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(16 * t + lr) * KROW + 8 * lg]);
-      sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    for (int g = 0; g < NQ; ++g) {
+      // S^T sub-tile t: lane holds S^T[key 16t + 4lg + i][query lr of group g]
+      f32x4 sacc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(16 * t + lr) * KROW + 8 * lg]);
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      // the running max stays in raw-score units (scale > 0): one fma per score folds the scale
+      // and the max subtraction; only the last, partial key tile pays for the mask
+      if (key0 + KTL > lk) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (key0 + 16 * t + 4 * lg + i >= lk) sacc[t][i] = -INFINITY;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sacc[t][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m_run[g], mx);
+      const float alpha = exp2f((m_run[g] - mnew) * scale_log2);
+      m_run[g] = mnew;
+      const float mneg = -mnew * scale_log2;
+      bf16x8 pf[NS];
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(fmaf(sacc[t][i], scale_log2, mneg));
+          ps += p;
+          pf[t >> 1][(t & 1) * 4 + i] = (bf16)p;
+        }
+      l_part[g] = l_part[g] * alpha + ps;
+#pragma unroll
+      for (int u = 0; u < NDT; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) oacc[g][u][i] *= alpha;
+      // O^T[d][q] += sum_k V^T[d][key(k)] P^T[key(k)][q]
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int u = 0; u < NDT; ++u) {
+          const bf16* vr = &Vt[(16 * u + lr) * VROW + 32 * s + 4 * lg];
+          const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr);
+          const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 16);
+          const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          oacc[g][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s], oacc[g][u], 0, 0, 0);
+        }
     }
-    float mx = -INFINITY;
+  }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float sv = (key0 + 16 * t + 4 * lg + i < lk) ? sacc[t][i] * scale_log2 : -INFINITY;
-        sacc[t][i] = sv;
-        mx = fmaxf(mx, sv);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - mnew);
-    m_run = mnew;
-    bf16x8 pf[2];
-    float ps = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = exp2f(sacc[t][i] - mnew);
-        ps += p;
-        pf[t >> 1][(t & 1) * 4 + i] = (bf16)p;
-      }
-    l_part = l_part * alpha + ps;
-#pragma unroll
-    for (int u = 0; u < NDT; ++u)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) oacc[u][i] *= alpha;
-    // O^T[d][q] += sum_k V^T[d][key(k)] P^T[key(k)][q]
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
+  for (int g = 0; g < NQ; ++g) {
+    float l = l_part[g];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+    const int myq = q0 + (wave * NQ + g) * 16 + lr;
+    if (myq < lq) {
+      bf16* orow = o + ((long)b * lq + myq) * ldo + h * DH;
 #pragma unroll
       for (int u = 0; u < NDT; ++u) {
-        const bf16* vr = &Vt[(16 * u + lr) * VROW + 32 * s + 4 * lg];
-        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr);
-        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 16);
-        const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        oacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[s], oacc[u], 0, 0, 0);
+        bf16x4 r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = (bf16)(oacc[g][u][i] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * u + 4 * lg) = r;
       }
-  }
-  float l = l_part;
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  const float inv = 1.f / l;
-  if (myq < lq) {
-    bf16* orow = o + ((long)b * lq + myq) * ldo + h * DH;
-#pragma unroll
-    for (int u = 0; u < NDT; ++u) {
-      bf16x4 r;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = (bf16)(oacc[u][i] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 16 * u + 4 * lg) = r;
     }
   }
 }
@@ -828,14 +852,19 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
     // small heads: register-resident P (A/B switch: RDEIC_ATTN_SMALL=0 -> generic kernel)
     static const bool small_on = !getenv("RDEIC_ATTN_SMALL") || atoi(getenv("RDEIC_ATTN_SMALL")) != 0;
     if ((dh == 16 || dh == 32) && small_on && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0) {
-      dim3 grid((lq + QT - 1) / QT, batch * heads);
       const float sl2 = scale * 1.4426950408889634f;
-      if (dh == 16)
-        hipLaunchKernelGGL(attn_small_kernel<16>, grid, dim3(256), 0, s, (const bf16*)q, ldq, (const bf16*)k, ldk,
-                           (const bf16*)v, ldv, (bf16*)o, ldo, heads, lq, lk, sl2, kv_bcast);
-      else
-        hipLaunchKernelGGL(attn_small_kernel<32>, grid, dim3(256), 0, s, (const bf16*)q, ldq, (const bf16*)k, ldk,
-                           (const bf16*)v, ldv, (bf16*)o, ldo, heads, lq, lk, sl2, kv_bcast);
+      // RDEIC_ATTN_SMALL=2: 2 query groups per wave over 128-key tiles on long sequences (A/B: 2.38 vs
+      // 2.22 ms/step for the default 1 x 64 — the kernel is VALU-bound on the softmax, not on staging)
+      const bool big = lq >= 1024 && getenv("RDEIC_ATTN_SMALL") && atoi(getenv("RDEIC_ATTN_SMALL")) == 2;
+#define SMALL_LAUNCH(D, NQ, KTL)                                                                                  \
+  hipLaunchKernelGGL((attn_small_kernel<D, NQ, KTL>), dim3((lq + 64 * NQ - 1) / (64 * NQ), batch * heads),       \
+                     dim3(256), 0, s, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, \
+                     heads, lq, lk, sl2, kv_bcast)
+      if (dh == 16 && big) SMALL_LAUNCH(16, 2, 128);
+      else if (dh == 16) SMALL_LAUNCH(16, 1, 64);
+      else if (big) SMALL_LAUNCH(32, 2, 128);
+      else SMALL_LAUNCH(32, 1, 64);
+#undef SMALL_LAUNCH
       return launch_status();
     }
   }

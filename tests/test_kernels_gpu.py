@@ -144,7 +144,7 @@ def _ref_attn(q, k, v, heads, dh, scale):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("heads,dh,lq,lk", [(5, 64, 256, 256), (4, 16, 300, 300), (10, 64, 64, 77), (16, 16, 64, 77),
-                                           (4, 16, 4096, 4096), (8, 32, 130, 200),
+                                           (4, 16, 4096, 4096), (8, 32, 130, 200), (2, 16, 1100, 77), (2, 32, 1030, 300),
                                            (20, 64, 100, 33)])
 def test_attention(gpu, dtype, heads, dh, lq, lk):
     from rdeic_amd import ops
