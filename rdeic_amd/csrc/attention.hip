@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m_run[g], mx);
-      const float alpha = exp2f((m_run[g] - mnew) * scale_log2);
+      const float alpha = __builtin_amdgcn_exp2f((m_run[g] - mnew) * scale_log2);
       m_run[g] = mnew;
       const float mneg = -mnew * scale_log2;
       bf16x8 pf[NS];
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(fmaf(sacc[t][i], scale_log2, mneg));
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[t][i], scale_log2, mneg));
           ps += p;
           pf[t >> 1][(t & 1) * 4 + i] = (bf16)p;
         }
