@@ -203,10 +203,16 @@ class WorkerPool {
   }
   void run(int32_t count, int32_t threads, const std::function<void(int32_t)>& f) {
     std::lock_guard<std::mutex> job(job_mu_);
-    const int32_t helpers = std::max(0, std::min(threads, count) - 1);
+    int32_t helpers = std::max(0, std::min(threads, count) - 1);
     while ((int32_t)workers_.size() < helpers) {
       const int32_t id = (int32_t)workers_.size();
-      std::thread(&WorkerPool::loop, this, id).detach();
+      try {
+        workers_.reserve(workers_.size() + 1);
+        std::thread(&WorkerPool::loop, this, id).detach();
+      } catch (...) {
+        helpers = (int32_t)workers_.size();  // out of threads: run with what exists
+        break;
+      }
       workers_.push_back(id);
     }
     {
@@ -257,6 +263,21 @@ class WorkerPool {
   uint64_t gen_ = 0;
 };
 
+// Every extern "C" body runs under guard(): no C++ exception may cross the C ABI (ctypes would
+// see std::terminate -> SIGABRT). Allocation failure maps to -ENOSPC, anything else to -EINVAL.
+template <typename F>
+int guard(F&& f) noexcept {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return RDEIC_ENOSPC;
+  } catch (...) {
+    return RDEIC_EINVAL;
+  }
+}
+
+// f(i) must not throw (callers catch inside); thread creation failure degrades to running the
+// remaining items on the calling thread.
 template <typename F>
 void parallel_for(int32_t count, int32_t threads, F&& f) {
   if (threads <= 1 || count <= 1) {
@@ -331,7 +352,7 @@ int rdeic_version(void) { return 1; }
 // number of entry points declared in include/rdeic_hip.h (checked by tests/test_abi.py)
 int rdeic_abi_count(void) { return 49; }
 
-int rdeic_pmf_to_quantized_cdf(const float* pmf, int32_t n, int32_t precision, uint32_t* cdf_out) {
+static int pmf_to_quantized_cdf_impl(const float* pmf, int32_t n, int32_t precision, uint32_t* cdf_out) {
   if (!pmf || !cdf_out || n <= 0 || precision <= 0 || precision > 24) return RDEIC_EINVAL;
   for (int32_t i = 0; i < n; ++i)
     if (!(pmf[i] >= 0.f) || !std::isfinite(pmf[i])) return RDEIC_EINVAL;
@@ -366,9 +387,12 @@ int rdeic_pmf_to_quantized_cdf(const float* pmf, int32_t n, int32_t precision, u
   return RDEIC_OK;
 }
 
-int rdeic_build_gaussian_tables(const float* pmf, const int32_t* pmf_len, int32_t levels, int32_t pmf_ld, int32_t* cdf,
-                                int32_t cdf_ld, int32_t* cdf_len, void* reserved) {
-  (void)reserved;
+int rdeic_pmf_to_quantized_cdf(const float* pmf, int32_t n, int32_t precision, uint32_t* cdf_out) {
+  return guard([&] { return pmf_to_quantized_cdf_impl(pmf, n, precision, cdf_out); });
+}
+
+static int build_gaussian_tables_impl(const float* pmf, const int32_t* pmf_len, int32_t levels, int32_t pmf_ld,
+                                      int32_t* cdf, int32_t cdf_ld, int32_t* cdf_len) {
   if (!pmf || !pmf_len || !cdf || !cdf_len || levels <= 0) return RDEIC_EINVAL;
   std::vector<float> row;
   std::vector<uint32_t> q;
@@ -378,7 +402,7 @@ int rdeic_build_gaussian_tables(const float* pmf, const int32_t* pmf_len, int32_
     // pmf row: L probabilities followed by the tail mass at column L
     row.assign(pmf + (size_t)i * pmf_ld, pmf + (size_t)i * pmf_ld + L + 1);
     q.assign((size_t)L + 2, 0u);
-    int rc = rdeic_pmf_to_quantized_cdf(row.data(), L + 1, kPrecision, q.data());
+    int rc = pmf_to_quantized_cdf_impl(row.data(), L + 1, kPrecision, q.data());
     if (rc) return rc;
     int32_t* out = cdf + (size_t)i * cdf_ld;
     for (int32_t j = 0; j < cdf_ld; ++j) out[j] = j < L + 2 ? (int32_t)q[j] : 0;
@@ -387,38 +411,42 @@ int rdeic_build_gaussian_tables(const float* pmf, const int32_t* pmf_len, int32_
   return RDEIC_OK;
 }
 
+int rdeic_build_gaussian_tables(const float* pmf, const int32_t* pmf_len, int32_t levels, int32_t pmf_ld, int32_t* cdf,
+                                int32_t cdf_ld, int32_t* cdf_len, void* reserved) {
+  (void)reserved;
+  return guard([&] { return build_gaussian_tables_impl(pmf, pmf_len, levels, pmf_ld, cdf, cdf_ld, cdf_len); });
+}
+
 int rdeic_rans_encode(const int32_t* sym, const int32_t* idx, size_t n, const int32_t* cdf, int32_t cdf_ld,
                       const int32_t* cdf_len, const int32_t* offset, int32_t levels, uint8_t* out, size_t cap,
                       size_t* out_len) {
   if ((!sym || !idx) && n) return RDEIC_EINVAL;
   if (!cdf || !cdf_len || !offset || !out || !out_len || levels <= 0) return RDEIC_EINVAL;
-  try {
+  return guard([&] {
     std::vector<RansSym> syms;
     std::vector<uint32_t> words;
     return rans_encode_impl(sym, idx, n, cdf, cdf_ld, cdf_len, offset, levels, out, cap, out_len, syms, words);
-  } catch (const std::bad_alloc&) {
-    return RDEIC_ENOSPC;
-  }
+  });
 }
 
 int rdeic_rans_encode_batch(int32_t count, const int32_t* sym, const int32_t* idx, size_t n_per, size_t stride,
                             const int32_t* cdf, int32_t cdf_ld, const int32_t* cdf_len, const int32_t* offset,
                             int32_t levels, uint8_t* out, size_t cap_per, size_t* out_len, int32_t threads) {
   if (count <= 0 || !sym || !idx || !out || !out_len) return RDEIC_EINVAL;
-  std::vector<int> rc(count, 0);
-  parallel_for(count, threads, [&](int32_t i) {
-    try {
-      std::vector<RansSym> syms;
-      std::vector<uint32_t> words;
-      rc[i] = rans_encode_impl(sym + i * stride, idx + i * stride, n_per, cdf, cdf_ld, cdf_len, offset, levels,
-                               out + i * cap_per, cap_per, &out_len[i], syms, words);
-    } catch (const std::bad_alloc&) {
-      rc[i] = RDEIC_ENOSPC;
-    }
+  return guard([&] {
+    std::vector<int> rc(count, 0);
+    parallel_for(count, threads, [&](int32_t i) {
+      rc[i] = guard([&] {
+        std::vector<RansSym> syms;
+        std::vector<uint32_t> words;
+        return rans_encode_impl(sym + i * stride, idx + i * stride, n_per, cdf, cdf_ld, cdf_len, offset, levels,
+                                out + i * cap_per, cap_per, &out_len[i], syms, words);
+      });
+    });
+    for (int v : rc)
+      if (v) return v;
+    return (int)RDEIC_OK;
   });
-  for (int v : rc)
-    if (v) return v;
-  return RDEIC_OK;
 }
 
 void* rdeic_rans_dec_open(const uint8_t* data, size_t len) {
@@ -426,7 +454,12 @@ void* rdeic_rans_dec_open(const uint8_t* data, size_t len) {
   RansDecoder* d = new (std::nothrow) RansDecoder();
   if (!d) return nullptr;
   const size_t nw = len / 4;
-  d->words.resize(nw);
+  try {
+    d->words.resize(nw);
+  } catch (...) {
+    delete d;
+    return nullptr;
+  }
   if (nw) memcpy(d->words.data(), data, nw * 4);
   if (len % 4 != 0 || nw < 2) {
     d->bad = true;
@@ -440,22 +473,26 @@ void* rdeic_rans_dec_open(const uint8_t* data, size_t len) {
 int rdeic_rans_decode(void* handle, const int32_t* idx, size_t n, const int32_t* cdf, int32_t cdf_ld,
                       const int32_t* cdf_len, const int32_t* offset, int32_t levels, int32_t* out) {
   if (!handle || (!idx && n) || (!out && n) || !cdf || !cdf_len || !offset) return RDEIC_EINVAL;
-  return rans_decode_impl((RansDecoder*)handle, idx, n, cdf, cdf_ld, cdf_len, offset, levels, out);
+  return guard([&] { return rans_decode_impl((RansDecoder*)handle, idx, n, cdf, cdf_ld, cdf_len, offset, levels, out); });
 }
 
 int rdeic_rans_decode_batch(int32_t count, void** handles, const int32_t* idx, size_t n_per, size_t stride,
                             const int32_t* cdf, int32_t cdf_ld, const int32_t* cdf_len, const int32_t* offset,
                             int32_t levels, int32_t* out, int32_t threads) {
   if (count <= 0 || !handles || !idx || !out) return RDEIC_EINVAL;
-  std::vector<int> rc(count, 0);
-  parallel_for(count, threads, [&](int32_t i) {
-    rc[i] = handles[i] ? rans_decode_impl((RansDecoder*)handles[i], idx + i * stride, n_per, cdf, cdf_ld, cdf_len,
-                                          offset, levels, out + i * stride)
-                       : RDEIC_EINVAL;
+  return guard([&] {
+    std::vector<int> rc(count, 0);
+    parallel_for(count, threads, [&](int32_t i) {
+      rc[i] = handles[i] ? guard([&] {
+        return rans_decode_impl((RansDecoder*)handles[i], idx + i * stride, n_per, cdf, cdf_ld, cdf_len, offset,
+                                levels, out + i * stride);
+      })
+                         : (int)RDEIC_EINVAL;
+    });
+    for (int v : rc)
+      if (v) return v;
+    return (int)RDEIC_OK;
   });
-  for (int v : rc)
-    if (v) return v;
-  return RDEIC_OK;
 }
 
 void rdeic_rans_dec_close(void* handle) { delete (RansDecoder*)handle; }

@@ -21,9 +21,28 @@ host steps. tests/test_plan_gpu.py checks replay == eager bit for bit.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import _lib, ops
+
+# MemPool lifetime. A plan's pool must outlive every tensor allocated from it: returning a block to
+# a destroyed pool aborts inside the caching allocator (a noexcept path, so SIGABRT). Models, plans
+# and their tensors form reference cycles, so the cyclic GC frees them in arbitrary order and at
+# arbitrary points (it once ran inside another plan's recording). Pools are therefore owned by this
+# registry, not by the plan, and are destroyed only by _sweep_pools() (called when a new plan is
+# made, never inside a pool context) once their plan is gone and no block of theirs is allocated.
+_POOLS: list = []  # [(weakref to LaunchPlan, MemPool)]
+
+
+def _pool_in_use(pool) -> bool:
+    return any(seg["allocated_size"] for seg in torch.cuda.memory_snapshot(pool.id))
+
+
+def _sweep_pools() -> None:
+    keep = [(ref, pool) for ref, pool in _POOLS if ref() is not None or _pool_in_use(pool)]
+    _POOLS[:] = keep  # the dropped pools are destroyed here, with no pool routing allocations
 
 
 class _HostStep:
@@ -54,7 +73,9 @@ def host_step(fn) -> None:
 class LaunchPlan:
     def __init__(self):
         self.calls = []
+        _sweep_pools()
         self.pool = torch.cuda.MemPool()
+        _POOLS.append((weakref.ref(self), self.pool))
         self.out = None
 
     def record(self, fn, *args):

@@ -67,3 +67,28 @@ def test_codec_plans_match_eager(gpu):
     # one group (no interleave) gives the same bytes
     m.preprocess_model.coder_groups = 1
     assert m.compress_images(imgs) == bodies_e
+
+
+def test_plan_pools_survive_cyclic_gc(gpu):
+    """A plan and its tensors in a reference cycle, collected by a GC pass that runs inside another
+    plan's recording (what aborted the round-1 driver run): the pool must outlive its tensors, and
+    dead pools with no live block are released when the next plan is made."""
+    import gc
+
+    from rdeic_amd import plan
+
+    class Owner:
+        pass
+
+    for _ in range(3):
+        o, p = Owner(), plan.LaunchPlan()
+        o.plan, p.owner = p, o  # cycle: only the cyclic GC frees it
+        o.t = p.record(lambda: torch.ones(1 << 20, device="cuda"))
+        del o, p
+    live = plan.LaunchPlan()
+    out = live.record(lambda: (gc.collect(), torch.full((1 << 20,), 2.0, device="cuda"))[1])
+    torch.cuda.synchronize()
+    assert float(out.sum()) == 2.0 * (1 << 20)
+    plan.LaunchPlan()  # sweeps: the three collected plans' pools are free now
+    dead = [pool for ref, pool in plan._POOLS if ref() is None]
+    assert len(dead) <= 1, len(dead)  # at most the plan made just above

@@ -70,14 +70,8 @@ def main():
         flops = 2.0 * B * ho * wo * cout * cin * k * k
         outs, r = {}, dict(name=name)
         for t in tiles:
-            ops.AUTOTUNE = True
-            ops.TILE_CANDIDATES = (t,) if t >= 0 else ()
-            ops._TILE_CACHE.clear()
-            if t < 0:
-                ops.AUTOTUNE = False
-                ops.set_conv_option(5, 0)
-            else:
-                ops.set_conv_option(5, 1)
+            ops.FORCE_TILE = t if t >= 0 else None
+            ops.set_conv_option(5, 0 if t < 0 else 1)
             fn = lambda: ops.conv2d(x, p, x2=x2, up2=bool(up2), res=res_t, act=ops.SILU, **kw)  # noqa: E731
             outs[t] = fn()
             torch.cuda.synchronize()
@@ -89,7 +83,7 @@ def main():
             r["maxdiff"] = {t: (ref.float() - o.float()).abs().max().item() for t, o in outs.items()}
         print(json.dumps(r), flush=True)
     ops.set_conv_option(5, 1)
-    ops.AUTOTUNE = True
+    ops.FORCE_TILE = None
 
 
 if __name__ == "__main__":

@@ -7,7 +7,8 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 if [ "${2:-tests}" = "tests" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+  # exactly the driver's command (no extra flags or env)
+  timeout -k 10 600 python3 -m pytest tests/ -x -q -m gpu > $O/pytest.log 2>&1
   echo "tests ok"
   timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
   echo "smoke ok"
