@@ -49,7 +49,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=16, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU per step (when --global-batch is unset)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="images per step over all ranks, sharded contiguously by parallel.shard "
+                         "(config 4: 128 on 8 GPUs); default --batch x world")
+    ap.add_argument("--bpp-sweep", default=None,
+                    help="comma list of target bpp (config 4: 0.04,0.08,0.12); each point re-initialises the "
+                         "synthetic rate layers with weights.rate_gain_for_bpp and is timed on its own; "
+                         "value/roofline come from the point nearest 0.08")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--ddim-steps", type=int, default=2, help="relay sampler steps")
     ap.add_argument("--sampler", default="ddim", choices=["ddim", "ddpm"],
@@ -78,12 +85,22 @@ def main():
     rank, world, local = parallel.init_from_env()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    B, S = args.batch, args.size
+    S = args.size
+    G = args.global_batch if args.global_batch is not None else args.batch * world
+    g0, g1 = parallel.shard(G, rank, world)  # this rank's contiguous slice of the global batch
+    B = g1 - g0
+    if B < 1:
+        raise SystemExit(f"global batch {G} leaves rank {rank} of {world} without images")
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     from rdeic_amd import weights as W
-    rate_gain = W.RATE_GAIN_BPP008 if args.rate_gain is None else args.rate_gain
-    model = RDEIC(compute_dtype=dtype, device=dev).init_synthetic(rate_gain=rate_gain)
-    model.preprocess_model.update(force=True)
+    if args.bpp_sweep:
+        targets = [float(v) for v in args.bpp_sweep.split(",")]
+        points = [(t, W.rate_gain_for_bpp(t)) for t in targets]
+    else:
+        points = [(None, W.RATE_GAIN_BPP008 if args.rate_gain is None else args.rate_gain)]
+    # the headline (and profiled) point: config 2's ~0.08 bpp when the sweep holds it
+    main_i = min(range(len(points)), key=lambda i: abs((points[i][0] or 0.08) - 0.08))
+    model = RDEIC(compute_dtype=dtype, device=dev)
     if args.coder_groups is not None:
         model.preprocess_model.coder_groups = args.coder_groups
     if args.no_plans:
@@ -91,9 +108,8 @@ def main():
     if args.no_geglu_fuse:
         ops.GEGLU_FUSED = False
 
-    g0 = rank * B  # global image indices of this rank's shard (weak scaling: B per GPU)
-    imgs = torch.from_numpy(np.stack([synth_image(S, S, 231 + g0 + i) for i in range(B)])).to(dev)
-    draws = [relay_noise((1, 4, S // 8, S // 8), 231 + g0 + i, args.ddim_steps) for i in range(B)]
+    imgs = torch.from_numpy(np.stack([synth_image(S, S, 231 + g) for g in range(g0, g1)])).to(dev)
+    draws = [relay_noise((1, 4, S // 8, S // 8), 231 + g, args.ddim_steps) for g in range(g0, g1)]
     noise = torch.cat([d[0] for d in draws])
     step_noise = torch.cat([d[1] for d in draws], 1) if args.sampler == "ddpm" else None
     ctx = synth_context().to(dev)
@@ -107,32 +123,42 @@ def main():
         rows = torch.tensor([[len(b) * 8.0 / (S * S), float(len(b)),
                               10 * math.log10(255.0 ** 2 / max(float(v), 1e-10)), float(v), 1.0, float(rank)]
                              for b, v in zip(bodies, m)], dtype=torch.float32, device=dev)
-        return parallel.gather_metrics(rows)
+        return parallel.gather_metrics(rows, G)
 
-    for _ in range(args.warmup):
-        step()
-    if not args.no_roofline:
-        # native launch profiler: the launchers record HIP events on their own stream for one launch
-        # in --prof-every of each kind (an event pair is two queue markers, i.e. GPU time)
-        ops.prof_start(2048 * max(1, args.steps) + 1024, args.prof_every)
-    parallel.barrier(dev)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        metrics = step()
-    parallel.barrier(dev)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    prof = None
-    if not args.no_roofline:
-        ops.prof_stop()
-        prof = ops.prof_read()
-    elapsed = parallel.max_over_ranks(elapsed, dev)
-    total_images = B * world * args.steps
-    value = total_images / elapsed
+    results = []
+    for i, (target, rate_gain) in enumerate(points):
+        model.init_synthetic(rate_gain=rate_gain)
+        model.preprocess_model.update(force=True)
+        for _ in range(args.warmup):
+            step()
+        profiled = i == main_i and not args.no_roofline
+        if profiled:
+            # native launch profiler: the launchers record HIP events on their own stream for one launch
+            # in --prof-every of each kind (an event pair is two queue markers, i.e. GPU time)
+            ops.prof_start(2048 * max(1, args.steps) + 1024, args.prof_every)
+        parallel.barrier(dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            metrics = step()
+        parallel.barrier(dev)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        prof = None
+        if profiled:
+            ops.prof_stop()
+            prof = ops.prof_read()
+        elapsed = parallel.max_over_ranks(elapsed, dev)
+        mrows = metrics.cpu().numpy()
+        results.append({"target_bpp": target, "rate_gain": rate_gain, "elapsed": elapsed, "prof": prof,
+                        "mean_bpp": float(mrows[:, 0].mean()), "mean_psnr_db": float(mrows[:, 2].mean()),
+                        "images": int(mrows.shape[0])})
+    parallel.finish()  # every rank leaves the group before rank 0's CPU-baseline leg
     if rank != 0:
         return
-
+    r = results[main_i]
+    elapsed, prof, rate_gain = r["elapsed"], r["prof"], r["rate_gain"]
+    value = G * args.steps / elapsed
     roof = None
     if prof and "conv" in prof:
         n, flops, ms = prof["conv"]
@@ -143,6 +169,7 @@ def main():
                 "traffic": conv_traffic(), "launches_per_step": round(n / args.steps, 1),
                 "sampling": f"launches >= 50 GFLOP always timed, smaller ones 1 in {args.prof_every} (weighted)",
                 "avg_launch_us": round(ms * 1e3 / max(1, n), 2), "ms_per_step": round(ms / args.steps, 3),
+                "flops_per_step": round(flops / args.steps),
                 "kernel_share_of_step": round(ms * 1e-3 / elapsed, 4)}
         # secondary kernels the north star names: attention on MFMA, GroupNorm on HBM
         sec = {}
@@ -160,7 +187,6 @@ def main():
                              "frac": round(a / PEAK_HBM_GBS, 4), "launches_per_step": round(cnt / args.steps, 1),
                              "ms_per_step": round(kms / args.steps, 3)}
         roof["secondary"] = sec
-    mrows = metrics.cpu().numpy()
     cpu = None
     if not args.no_cpu_baseline:
         try:
@@ -174,15 +200,21 @@ def main():
         "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded images, random-init weights)",
-        "config": {"workload": f"{cfg_name}: batch {B}/GPU {S}x{S}, {args.ddim_steps}-step relay "
+        "config": {"workload": f"{cfg_name}: global batch {G} ({G // world}{'+' if G % world else ''}/GPU) {S}x{S}, "
+                               f"{args.ddim_steps}-step relay "
                                f"{'DDIM' if args.sampler == 'ddim' else 'spaced DDPM'}, "
-                               f"encode+entropy-code+decode+VAE-decode", "global_batch": B * world,
+                               f"encode+entropy-code+decode+VAE-decode", "global_batch": G,
                    "image_size": S, "ddim_steps": args.ddim_steps, "sampler": args.sampler, "parallelism": f"dp{world}", "rate_gain": rate_gain,
-                   "mean_bpp": round(float(mrows[:, 0].mean()), 4),
-                   "mean_psnr_db": round(float(mrows[:, 2].mean()), 2)},
+                   "mean_bpp": round(r["mean_bpp"], 4), "mean_psnr_db": round(r["mean_psnr_db"], 2)},
         "roofline": roof,
         "cpu_baseline": cpu,
     }
+    if args.bpp_sweep:
+        line["bpp_sweep"] = [{"target_bpp": p["target_bpp"], "rate_gain": p["rate_gain"],
+                              "achieved_mean_bpp": round(p["mean_bpp"], 4), "mean_psnr_db": round(p["mean_psnr_db"], 2),
+                              "images_per_s": round(G * args.steps / p["elapsed"], 3),
+                              "ms_per_step": round(p["elapsed"] / args.steps * 1e3, 2), "images": p["images"]}
+                             for p in results]
     print(json.dumps(line), flush=True)
 
 

@@ -14,10 +14,10 @@ from . import model_ref as M
 
 
 def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads: int = None,
-                     rate_gain: float = 1.0):
+                     rate_gain: float = 1.0, warmup: int = 1):
     from rdeic_amd.synthetic import sampler_noise, synth_context, synth_image  # test-input generators
     if threads is None:
-        threads = min(16, os.cpu_count() or 1)
+        threads = len(os.sched_getaffinity(0))  # every host core this process may run on
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
@@ -27,6 +27,8 @@ def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads
         imgs = [synth_image(size, size, 231 + i) for i in range(n_images)]
         noises = [sampler_noise((1, 4, size // 8, size // 8), 231 + i)[1] for i in range(n_images)]
         with torch.no_grad():
+            for _ in range(warmup):  # untimed: oneDNN primitive creation, allocator growth
+                M.codec_image(sd, tables, imgs[0], ctx, noises[0], steps=steps, coder="c")
             t0 = time.perf_counter()
             for img, nz in zip(imgs, noises):
                 M.codec_image(sd, tables, img, ctx, nz, steps=steps, coder="c")
@@ -34,8 +36,9 @@ def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads
     finally:
         torch.set_num_threads(prev)
     return {"value": round(n_images / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n_images} image(s) {size}x{size}, {steps} DDIM steps, full encode->code->"
-                      f"relay->decode on torch-CPU fp32 ({dt:.1f} s)"}
+            "sample": f"{n_images} image(s) {size}x{size} after {warmup} untimed warm-up image(s), {steps} DDIM "
+                      f"steps, full encode->code->relay->decode on torch-CPU fp32, "
+                      f"torch.set_num_threads({threads}) = len(os.sched_getaffinity(0)) ({dt:.1f} s)"}
 
 
 if __name__ == "__main__":

@@ -37,14 +37,26 @@ def shard(global_batch: int, rank: int, world: int) -> Tuple[int, int]:
     return start, start + base + (1 if rank < rem else 0)
 
 
-def gather_metrics(rows: torch.Tensor) -> torch.Tensor:
-    """All-gather [B_local, k] fp32 metric rows -> [world * B_local, k] (equal shards)."""
+def gather_metrics(rows: torch.Tensor, global_batch: int = None) -> torch.Tensor:
+    """All-gather each rank's [B_local, k] fp32 metric rows -> [global_batch, k] in global image
+    order. Shards come from shard(global_batch, ...), so they may differ by one row: every rank
+    pads to the largest shard, ONE all_gather_into_tensor moves [world, B_max, k], and the padding
+    is dropped by the known shard sizes (no second collective for the sizes)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return rows
-    world = dist.get_world_size()
-    out = torch.empty((world * rows.shape[0], rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    dist.all_gather_into_tensor(out, rows.contiguous())
-    return out
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if global_batch is None:
+        global_batch = world * rows.shape[0]
+    sizes = [shard(global_batch, r, world) for r in range(world)]
+    if rows.shape[0] != sizes[rank][1] - sizes[rank][0]:
+        raise ValueError(f"rank {rank} holds {rows.shape[0]} rows, its shard of {global_batch} is {sizes[rank]}")
+    bmax = max(e - s for s, e in sizes)
+    send = rows.new_zeros((bmax, rows.shape[1]))
+    send[: rows.shape[0]] = rows
+    out = torch.empty((world * bmax, rows.shape[1]), dtype=rows.dtype, device=rows.device)
+    dist.all_gather_into_tensor(out, send)
+    out = out.view(world, bmax, rows.shape[1])
+    return torch.cat([out[r, : e - s] for r, (s, e) in enumerate(sizes)])
 
 
 def max_over_ranks(value: float, device) -> float:
@@ -53,6 +65,12 @@ def max_over_ranks(value: float, device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def finish() -> None:
+    """Leave the process group (every rank, before any rank-local tail work such as the CPU baseline)."""
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def barrier(device=None):

@@ -41,3 +41,16 @@ def test_ddim_timesteps():
     from rdeic_amd.ddim_sampler_relay import make_ddim_timesteps
     assert make_ddim_timesteps(2, 300).tolist() == [1, 151]
     assert make_ddim_timesteps(5, 300).tolist() == [1, 61, 121, 181, 241]
+
+
+def test_rate_gain_calibration():
+    """bench.py --bpp-sweep's rate knob: the calibration table is monotone and the interpolation
+    returns its own points and stays between neighbours (rdeic_amd/weights.py)."""
+    from rdeic_amd import weights as W
+    pts = W.RATE_CALIBRATION_512
+    assert all(a[0] < b[0] and a[1] < b[1] for a, b in zip(pts, pts[1:]))
+    for g, b in pts:
+        assert abs(W.rate_gain_for_bpp(b) - g) < 1e-4
+    gains = [W.rate_gain_for_bpp(b) for b in (0.04, 0.08, 0.12)]
+    assert 0.36 < gains[0] < 0.37 and 0.40 < gains[1] < 0.405 and 0.42 < gains[2] < 0.43
+    assert W.rate_gain_for_bpp(0.001) == pts[0][0] and W.rate_gain_for_bpp(10.0) == pts[-1][0]

@@ -1,5 +1,6 @@
 """Data-parallel plumbing (rdeic_amd/parallel.py) on CPU with gloo, world_size 2: shards cover
-the global batch exactly once, the metric all-gather returns every rank's rows in rank order,
+the global batch exactly once, the metric all-gather returns every rank's rows in global image
+order (unequal shards included),
 and the timing reduction takes the max over ranks (bench.py's contract)."""
 import os
 import socket
@@ -19,24 +20,24 @@ def _free_port():
     return p
 
 
+G = 11
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     r, w, _ = parallel.init_from_env(backend="gloo")
     assert (r, w) == (rank, world)
-    s, e = parallel.shard(10, r, w)
+    s, e = parallel.shard(G, r, w)  # unequal shards when world does not divide G
     rows = torch.tensor([[float(i), float(r)] for i in range(s, e)], dtype=torch.float32)
-    # equal shards for the gather: pad to ceil(10/world)
-    per = -(-10 // w)
-    pad = torch.full((per - rows.shape[0], 2), -1.0)
-    g = parallel.gather_metrics(torch.cat([rows, pad]))
+    g = parallel.gather_metrics(rows, G)
     t = parallel.max_over_ranks(1.0 + r, torch.device("cpu"))
     parallel.barrier()
     q.put((r, g.tolist(), t))
-    torch.distributed.destroy_process_group()
+    parallel.finish()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_gloo_gather_and_max(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -50,10 +51,10 @@ def test_gloo_gather_and_max(world):
         assert p.exitcode == 0
     for r, g, t in res:
         assert t == float(world)
-        ids = [row[0] for row in g if row[0] >= 0]
-        assert ids == list(range(10))
-        owners = [int(row[1]) for row in g if row[0] >= 0]
-        assert owners == sorted(owners)
+        ids = [row[0] for row in g]
+        assert ids == list(range(G))  # global image order, padding dropped
+        owners = [int(row[1]) for row in g]
+        assert owners == [r for r in range(world) for _ in range(*parallel.shard(G, r, world))]
 
 
 def test_shard_partition():
