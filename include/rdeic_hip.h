@@ -228,6 +228,19 @@ int rdeic_rans_encode_batch(int32_t count, const int32_t* sym, const int32_t* id
                             size_t stride, const int32_t* cdf, int32_t cdf_ld, const int32_t* cdf_len,
                             const int32_t* offset, int32_t levels, uint8_t* out, size_t cap_per,
                             size_t* out_len, int32_t threads);
+/* The same streams from precomputed per-(row, value) encoder symbols: start, freq and the exact
+ * reciprocal of freq (Alverson; ryg_rans Rans64EncSymbolInit), so the flush is ONE reverse pass
+ * over the symbols with no 64-bit division and no intermediate symbol list. Tables are built once
+ * per GaussianConditional table set, are immutable and are shared by all threads (NULL on a bad
+ * table). rdeic_rans_encode_batch_t writes the bytes rdeic_rans_encode_batch writes;
+ * rdeic_rans_enc_quotient exposes one reciprocal division (floor(x / freq)) for tests. */
+void* rdeic_rans_enc_tables_create(const int32_t* cdf, int32_t cdf_ld, const int32_t* cdf_len,
+                                   const int32_t* offset, int32_t levels);
+void rdeic_rans_enc_tables_destroy(void* tables);
+int rdeic_rans_encode_batch_t(const void* tables, int32_t count, const int32_t* sym, const int32_t* idx,
+                              size_t n_per, size_t stride, uint8_t* out, size_t cap_per, size_t* out_len,
+                              int32_t threads);
+int rdeic_rans_enc_quotient(const void* tables, int32_t row, int32_t value, uint64_t x, uint64_t* q);
 void* rdeic_rans_dec_open(const uint8_t* data, size_t len);
 int rdeic_rans_decode(void* handle, const int32_t* idx, size_t n, const int32_t* cdf, int32_t cdf_ld,
                       const int32_t* cdf_len, const int32_t* offset, int32_t levels, int32_t* out);

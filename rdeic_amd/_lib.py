@@ -100,6 +100,10 @@ PROTOTYPES = {
     "rdeic_build_gaussian_tables": (C.c_int, [_p, _p, _i32, _i32, _p, _i32, _p, _p]),
     "rdeic_rans_encode": (C.c_int, [_p, _p, _sz, _p, _i32, _p, _p, _i32, _p, _sz, C.POINTER(_sz)]),
     "rdeic_rans_encode_batch": (C.c_int, [_i32, _p, _p, _sz, _sz, _p, _i32, _p, _p, _i32, _p, _sz, _p, _i32]),
+    "rdeic_rans_enc_tables_create": (_p, [_p, _i32, _p, _p, _i32]),
+    "rdeic_rans_enc_tables_destroy": (None, [_p]),
+    "rdeic_rans_encode_batch_t": (C.c_int, [_p, _i32, _p, _p, _sz, _sz, _p, _sz, _p, _i32]),
+    "rdeic_rans_enc_quotient": (C.c_int, [_p, _i32, _i32, C.c_uint64, C.POINTER(C.c_uint64)]),
     "rdeic_rans_dec_open": (_p, [_p, _sz]),
     "rdeic_rans_decode": (C.c_int, [_p, _p, _sz, _p, _i32, _p, _p, _i32, _p]),
     "rdeic_rans_decode_batch": (C.c_int, [_i32, _p, _p, _sz, _sz, _p, _i32, _p, _p, _i32, _p, _i32]),

@@ -71,6 +71,26 @@ class GaussianTables:
              self.cdf_ld, _np_ptr(self.cdf_length), None)
         self.offset = (-pmf_center).numpy().astype(np.int32)
         self._dev = None
+        self._enc = None
+
+    def encoder_tables(self) -> int:
+        """Handle of the precomputed encoder symbols (rdeic_rans_enc_tables_create), built once."""
+        if self._enc is None:
+            lib = _lib.load()
+            h = lib.rdeic_rans_enc_tables_create(_np_ptr(self.cdf), self.cdf_ld, _np_ptr(self.cdf_length),
+                                                 _np_ptr(self.offset), self.levels)
+            if not h:
+                raise ValueError("rdeic_rans_enc_tables_create rejected the CDF tables")
+            self._enc = h
+        return self._enc
+
+    def __del__(self):
+        try:
+            if self._enc:
+                _lib.load().rdeic_rans_enc_tables_destroy(self._enc)
+                self._enc = None
+        except Exception:
+            pass
 
     def device_scale_table(self, device) -> torch.Tensor:
         if self._dev is None or self._dev.device != torch.device(device):
@@ -97,17 +117,24 @@ def rans_encode(symbols: np.ndarray, indexes: np.ndarray, t: GaussianTables) -> 
     return out[:n.value].tobytes()
 
 
-def rans_encode_batch(symbols: np.ndarray, indexes: np.ndarray, t: GaussianTables, threads: int = None) -> List[bytes]:
-    """symbols / indexes [count, n] int32 -> one rANS stream per row (threads across rows)."""
+def rans_encode_batch(symbols: np.ndarray, indexes: np.ndarray, t: GaussianTables, threads: int = None,
+                      tabled: bool = True) -> List[bytes]:
+    """symbols / indexes [count, n] int32 -> one rANS stream per row (threads across rows).
+    tabled (default): one reverse pass on the precomputed encoder symbols (no divisions);
+    tabled=False: the two-pass restatement (BufferedRansEncoder's symbol list, then flush)."""
     sym = np.ascontiguousarray(symbols, dtype=np.int32)
     idx = np.ascontiguousarray(indexes, dtype=np.int32)
     count, n = sym.shape
     cap = 4 * (n * 4 + 16)
     out = np.empty((count, cap), dtype=np.uint8)
     lens = np.zeros(count, dtype=np.uint64)
-    call("rdeic_rans_encode_batch", count, _np_ptr(sym), _np_ptr(idx), n, n, _np_ptr(t.cdf), t.cdf_ld,
-         _np_ptr(t.cdf_length), _np_ptr(t.offset), t.levels, _np_ptr(out), cap, _np_ptr(lens),
-         threads or default_threads())
+    if tabled:
+        call("rdeic_rans_encode_batch_t", t.encoder_tables(), count, _np_ptr(sym), _np_ptr(idx), n, n, _np_ptr(out),
+             cap, _np_ptr(lens), threads or default_threads())
+    else:
+        call("rdeic_rans_encode_batch", count, _np_ptr(sym), _np_ptr(idx), n, n, _np_ptr(t.cdf), t.cdf_ld,
+             _np_ptr(t.cdf_length), _np_ptr(t.offset), t.levels, _np_ptr(out), cap, _np_ptr(lens),
+             threads or default_threads())
     return [out[i, :int(lens[i])].tobytes() for i in range(count)]
 
 

@@ -24,6 +24,7 @@
 #include <mutex>
 #include <cmath>
 #include <new>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -115,6 +116,117 @@ int rans_encode_impl(const int32_t* sym, const int32_t* idx, size_t n, const int
   *out_len = nbytes;
   if (nbytes > cap) return RDEIC_ENOSPC;
   memcpy(out, words.data() + wp, nbytes);
+  return RDEIC_OK;
+}
+
+// ---- encoder on precomputed symbol tables ------------------------------------
+// One entry per (cdf row, value): the rANS put x' = (x / freq) << 16 + x % freq + start done
+// without a 64-bit division, as q = mulhi(x, rcp) >> shift (Alverson's exact reciprocal, the
+// form of ryg_rans' Rans64EncSymbolInit), x' = x + bias + q * (2^16 - freq). For freq = 1 the
+// reciprocal is 2^64 - 1 with shift 0 (q = x - 1) and bias = start + 2^16 - 1. Exact for every
+// x < 2^63 (the encoder never holds more: x < freq << 47 before each put), so the bytes equal
+// rans_encode_impl's; tests/test_coders.py checks both the quotients and whole streams.
+struct EncSym {
+  uint64_t rcp;
+  uint32_t bias;
+  uint16_t freq;   // 1..65535 (a zero-width bin is never coded)
+  uint8_t shift;
+  uint8_t pad;
+};
+
+struct EncTables {
+  std::vector<EncSym> sym;         // row ci's entries at row_off[ci] .. row_off[ci] + cdf_len[ci] - 2
+  std::vector<int32_t> row_off, max_value, offset;
+  int32_t levels = 0;
+};
+
+EncSym make_enc_sym(uint32_t start, uint32_t freq) {
+  EncSym s{};
+  s.freq = (uint16_t)freq;
+  if (freq < 2) {
+    s.rcp = ~0ull;
+    s.shift = 0;
+    s.bias = start + (1u << kPrecision) - 1;
+  } else {
+    uint32_t sh = 0;
+    while (freq > (1u << sh)) ++sh;  // ceil(log2 freq)
+    const unsigned __int128 num = ((unsigned __int128)1 << (sh + 63)) + (freq - 1);
+    s.rcp = (uint64_t)(num / freq);
+    s.shift = (uint8_t)(sh - 1);
+    s.bias = start;
+  }
+  return s;
+}
+
+inline uint64_t enc_quot(uint64_t x, const EncSym& s) {
+  return (uint64_t)(((unsigned __int128)x * s.rcp) >> 64) >> s.shift;
+}
+
+// Words are written from the end of a per-thread buffer; it grows (keeping the tail) if a
+// stream ever needs more than the initial estimate.
+struct WordSink {
+  std::vector<uint32_t>& buf;
+  size_t wp;
+  explicit WordSink(std::vector<uint32_t>& b) : buf(b), wp(b.size()) {}
+  void emit(uint32_t w) {
+    if (wp == 0) grow();
+    buf[--wp] = w;
+  }
+  void grow() {
+    const size_t old = buf.size(), add = std::max<size_t>(old, 1024);
+    std::vector<uint32_t> nb(old + add);
+    memcpy(nb.data() + add, buf.data(), old * sizeof(uint32_t));
+    buf.swap(nb);
+    wp += add;
+  }
+};
+
+inline void enc_put(uint64_t& x, WordSink& ws, const EncSym& s) {
+  if ((x >> 47) >= s.freq) {  // x >= x_max = ((L >> 16) << 32) * freq = freq << 47
+    ws.emit((uint32_t)x);
+    x >>= 32;
+  }
+  x = x + s.bias + enc_quot(x, s) * ((1u << kPrecision) - s.freq);
+}
+
+inline void enc_put_bits(uint64_t& x, WordSink& ws, uint32_t v) {
+  if ((x >> 59) != 0) {  // bypass freq 2^12: x_max = 2^12 << 47
+    ws.emit((uint32_t)x);
+    x >>= 32;
+  }
+  x = (x << kBypassBits) | v;
+}
+
+// Same stream as rans_encode_impl in ONE reverse pass over the symbols: for symbol i the puts of
+// its bypass nibbles (last first), then of its nibble count (the remainder, then the 15s), then
+// of the symbol itself — exactly the reversed order of BufferedRansEncoder's list.
+int rans_encode_tab_impl(const EncTables& T, const int32_t* sym, const int32_t* idx, size_t n, uint8_t* out,
+                         size_t cap, size_t* out_len, std::vector<uint32_t>& buf) {
+  if (buf.size() < n / 2 + 256) buf.assign(n / 2 + 256, 0u);
+  WordSink ws(buf);
+  uint64_t x = kRansL;
+  for (size_t i = n; i-- > 0;) {
+    const int32_t ci = idx[i];
+    if (ci < 0 || ci >= T.levels) return RDEIC_EINVAL;
+    const int32_t max_value = T.max_value[ci];
+    int32_t value = sym[i] - T.offset[ci];
+    if (value < 0 || value >= max_value) {
+      const uint32_t raw = value < 0 ? (uint32_t)(-2 * (int64_t)value - 1) : (uint32_t)(2 * (int64_t)(value - max_value));
+      int32_t nb = 0;
+      while (nb < 8 && (raw >> (nb * kBypassBits)) != 0) ++nb;
+      for (int32_t j = nb; j-- > 0;) enc_put_bits(x, ws, (raw >> (j * kBypassBits)) & kBypassMax);
+      enc_put_bits(x, ws, (uint32_t)(nb % (int32_t)kBypassMax));
+      for (int32_t v = nb / (int32_t)kBypassMax; v-- > 0;) enc_put_bits(x, ws, kBypassMax);
+      value = max_value;
+    }
+    enc_put(x, ws, T.sym[(size_t)T.row_off[ci] + value]);
+  }
+  ws.emit((uint32_t)(x >> 32));
+  ws.emit((uint32_t)x);
+  const size_t nbytes = (ws.buf.size() - ws.wp) * 4;
+  *out_len = nbytes;
+  if (nbytes > cap) return RDEIC_ENOSPC;
+  memcpy(out, ws.buf.data() + ws.wp, nbytes);
   return RDEIC_OK;
 }
 
@@ -350,7 +462,7 @@ extern "C" {
 int rdeic_version(void) { return 1; }
 
 // number of entry points declared in include/rdeic_hip.h (checked by tests/test_abi.py)
-int rdeic_abi_count(void) { return 49; }
+int rdeic_abi_count(void) { return 53; }
 
 static int pmf_to_quantized_cdf_impl(const float* pmf, int32_t n, int32_t precision, uint32_t* cdf_out) {
   if (!pmf || !cdf_out || n <= 0 || precision <= 0 || precision > 24) return RDEIC_EINVAL;
@@ -447,6 +559,70 @@ int rdeic_rans_encode_batch(int32_t count, const int32_t* sym, const int32_t* id
       if (v) return v;
     return (int)RDEIC_OK;
   });
+}
+
+void* rdeic_rans_enc_tables_create(const int32_t* cdf, int32_t cdf_ld, const int32_t* cdf_len, const int32_t* offset,
+                                   int32_t levels) {
+  if (!cdf || !cdf_len || !offset || levels <= 0 || cdf_ld < 2) return nullptr;
+  EncTables* T = new (std::nothrow) EncTables();
+  if (!T) return nullptr;
+  try {
+    T->levels = levels;
+    T->row_off.resize(levels);
+    T->max_value.resize(levels);
+    T->offset.assign(offset, offset + levels);
+    size_t total = 0;
+    for (int32_t ci = 0; ci < levels; ++ci) {
+      const int32_t len = cdf_len[ci];
+      if (len < 2 || len > cdf_ld) throw std::invalid_argument("cdf_len");
+      T->row_off[ci] = (int32_t)total;
+      T->max_value[ci] = len - 2;
+      total += (size_t)len - 1;
+    }
+    T->sym.resize(total);
+    for (int32_t ci = 0; ci < levels; ++ci) {
+      const int32_t* row = cdf + (size_t)ci * cdf_ld;
+      for (int32_t v = 0; v <= T->max_value[ci]; ++v) {
+        const int32_t start = row[v], freq = row[v + 1] - row[v];
+        if (start < 0 || freq <= 0 || start + freq > (1 << kPrecision)) throw std::invalid_argument("cdf row");
+        T->sym[(size_t)T->row_off[ci] + v] = make_enc_sym((uint32_t)start, (uint32_t)freq);
+      }
+    }
+  } catch (...) {
+    delete T;
+    return nullptr;
+  }
+  return T;
+}
+
+void rdeic_rans_enc_tables_destroy(void* tables) { delete (EncTables*)tables; }
+
+int rdeic_rans_encode_batch_t(const void* tables, int32_t count, const int32_t* sym, const int32_t* idx, size_t n_per,
+                              size_t stride, uint8_t* out, size_t cap_per, size_t* out_len, int32_t threads) {
+  if (!tables || count <= 0 || ((!sym || !idx) && n_per) || !out || !out_len) return RDEIC_EINVAL;
+  const EncTables& T = *(const EncTables*)tables;
+  return guard([&] {
+    std::vector<int> rc(count, 0);
+    parallel_for(count, threads, [&](int32_t i) {
+      rc[i] = guard([&] {
+        thread_local std::vector<uint32_t> buf;
+        return rans_encode_tab_impl(T, sym + i * stride, idx + i * stride, n_per, out + i * cap_per, cap_per,
+                                    &out_len[i], buf);
+      });
+    });
+    for (int v : rc)
+      if (v) return v;
+    return (int)RDEIC_OK;
+  });
+}
+
+int rdeic_rans_enc_quotient(const void* tables, int32_t row, int32_t value, uint64_t x, uint64_t* q) {
+  if (!tables || !q) return RDEIC_EINVAL;
+  const EncTables& T = *(const EncTables*)tables;
+  if (row < 0 || row >= T.levels || value < 0 || value > T.max_value[row]) return RDEIC_EINVAL;
+  const EncSym& s = T.sym[(size_t)T.row_off[row] + value];
+  *q = s.freq < 2 ? x : enc_quot(x, s);  // freq 1 stores q = x - 1 with bias + 2^16 - 1; report x / 1
+  return RDEIC_OK;
 }
 
 void* rdeic_rans_dec_open(const uint8_t* data, size_t len) {

@@ -188,3 +188,33 @@ def test_golden_z_string(gold):
         idx = gold[f"img{i}_z_idx"].reshape(-1)
         assert coders.ac_encode_uniform(idx, 16384) == gold[f"img{i}_z_string"].tobytes()
         assert np.array_equal(coders.ac_decode_uniform(gold[f"img{i}_z_string"].tobytes(), idx.size, 16384), idx)
+
+
+def test_tabled_encoder_bytes_and_reciprocals(tables, gold):
+    """rdeic_rans_encode_batch_t (one reverse pass on precomputed reciprocal symbols) writes the
+    same streams as the two-pass restatement of BufferedRansEncoder, escapes and multi-nibble
+    bypass chains included, and every reciprocal division it uses is floor(x / freq) exactly,
+    over the whole valid state range x < freq << 47 (sampled, plus both ends)."""
+    import ctypes as C
+    from rdeic_amd import _lib
+    rng = np.random.default_rng(7)
+    n = 20000
+    idx = rng.integers(0, 64, size=(3, n)).astype(np.int32)
+    sym = (rng.random((3, n)) < 0.2).astype(np.int32) * rng.integers(-60, 60, size=(3, n)).astype(np.int32)
+    sym[0, :200] = rng.integers(-200000, 200000, size=200)
+    sym[1, :20] = 2 ** 30
+    sym[1, 20:40] = -2 ** 30
+    assert coders.rans_encode_batch(sym, idx, tables, threads=3, tabled=True) == \
+        coders.rans_encode_batch(sym, idx, tables, threads=3, tabled=False)
+    # the golden file's y string (the reference's call order) from the tabled path
+    y = coders.rans_encode_batch(gold["img0_symbols"][None], gold["img0_indexes"][None], tables)[0]
+    assert y == gold["img0_y_string"].tobytes()
+    lib, h, q = _lib.load(), tables.encoder_tables(), C.c_uint64()
+    for row in range(0, 64, 3):
+        L = int(tables.cdf_length[row])
+        for v in sorted({0, 1, L // 2, L - 3, L - 2}):
+            f = int(tables.cdf[row, v + 1] - tables.cdf[row, v])
+            xs = [1, 2 ** 31, (f << 47) - 1] + [int(x) for x in rng.integers(1, f << 47, size=64, dtype=np.uint64)]
+            for x in xs:
+                assert lib.rdeic_rans_enc_quotient(h, row, v, x, C.byref(q)) == 0
+                assert q.value == x // f, (row, v, f, x)
