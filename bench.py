@@ -125,8 +125,13 @@ def main():
                              for b, v in zip(bodies, m)], dtype=torch.float32, device=dev)
         return parallel.gather_metrics(rows, G)
 
+    def log(msg):  # progress on stderr (the JSON line is the only stdout)
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
     results = []
     for i, (target, rate_gain) in enumerate(points):
+        log(f"point {i + 1}/{len(points)}: rate_gain {rate_gain}, {args.warmup} warm-up + {args.steps} timed steps")
         model.init_synthetic(rate_gain=rate_gain)
         model.preprocess_model.update(force=True)
         for _ in range(args.warmup):
@@ -189,6 +194,7 @@ def main():
         roof["secondary"] = sec
     cpu = None
     if not args.no_cpu_baseline:
+        log("cpu baseline (oracle restatement on the host cores)")
         try:
             from oracle.bench_cpu import run_cpu_baseline
             cpu = run_cpu_baseline(size=S, steps=args.ddim_steps, rate_gain=rate_gain)

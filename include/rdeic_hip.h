@@ -71,6 +71,13 @@ typedef struct rdeic_conv_desc {
   int32_t out_f32;      /* bf16 mode only: write fp32 output (and read fp32 residual) */
   int32_t batch;        /* >1: batched GEMM (grid z); operand z starts at +z*{in,w,out}_bs elements */
   int64_t in_bs, w_bs, out_bs;
+  float* gn_part;       /* NULL, or GroupNorm statistics of the output in the partial format of
+                           rdeic_groupnorm_parts_ab (rdeic_groupnorm_parts_floats(n*ho*wo, cout, gn_hw)
+                           floats): fused into the LDS-DMA epilogue where the tile allows, else written
+                           by a separate pass. out_mode 0, batch 1 */
+  int32_t gn_hw;        /* pixels per image of the GroupNorm those statistics feed (divides n*ho*wo;
+                           differs from ho*wo when a linear's rows are an image's tokens) */
+  int32_t reserved;
 } rdeic_conv_desc;
 
 int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
@@ -112,6 +119,16 @@ int rdeic_set_conv_option(int32_t key, int32_t value);
  * ws: fp32 workspace of at least rdeic_groupnorm_ws_floats(n, hw, c) floats. */
 size_t rdeic_groupnorm_ws_floats(int32_t n, int32_t hw, int32_t c);
 /* The input is the channel concatenation of x0 [n][hw][ld0] (c0 ch) and, if c1 > 0, x1 (c1 ch). */
+/* GroupNorm affine from per-row-block partial sums (rdeic_conv_desc.gn_part): a 16-byte header
+ * whose first int32 is R = 64 (rows per partial; hw % 64 == 0), then [rows/64][c][2] fp32 (sum,
+ * sum of squares) in a canonical order independent of the conv tile (so the result is identical for
+ * every tile and batch size). Channels [0, c0) from p0, [c0, c0+c1) from p1 (a concat); sums in
+ * fp64 in a fixed order, var = E[x^2] - mean^2; writes ab like rdeic_groupnorm_stats.
+ * rdeic_groupnorm_parts_floats: buffer size for a [rows][c] tensor, 0 when hw % 64 != 0. */
+size_t rdeic_groupnorm_parts_floats(int64_t rows, int32_t c, int32_t hw);
+int rdeic_groupnorm_parts_ab(const float* p0, int32_t c0, const float* p1, int32_t c1, int32_t n, int32_t hw,
+                             int32_t groups, float eps, const float* gamma, const float* beta, float* ab,
+                             void* stream);
 int rdeic_groupnorm_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1, int32_t ld1,
                           int32_t n, int32_t hw, int32_t groups, float eps, const float* gamma, const float* beta,
                           float* ab, float* ws, int32_t dtype, void* stream);

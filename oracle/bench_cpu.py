@@ -13,11 +13,26 @@ import torch
 from . import model_ref as M
 
 
+def available_cores() -> int:
+    """Host cores this process can actually use: the CPU affinity set, capped by the cgroup's CPU
+    quota (cpu.max). On the GPU box the affinity set is the whole 256-thread host while the quota
+    is 16 CPUs; more threads than the quota only get throttled."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads: int = None,
                      rate_gain: float = 1.0, warmup: int = 1):
     from rdeic_amd.synthetic import sampler_noise, synth_context, synth_image  # test-input generators
     if threads is None:
-        threads = len(os.sched_getaffinity(0))  # every host core this process may run on
+        threads = available_cores()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
@@ -38,7 +53,8 @@ def run_cpu_baseline(size: int = 512, steps: int = 2, n_images: int = 1, threads
     return {"value": round(n_images / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{n_images} image(s) {size}x{size} after {warmup} untimed warm-up image(s), {steps} DDIM "
                       f"steps, full encode->code->relay->decode on torch-CPU fp32, "
-                      f"torch.set_num_threads({threads}) = len(os.sched_getaffinity(0)) ({dt:.1f} s)"}
+                      f"torch.set_num_threads({threads}) = available host cores (affinity {len(os.sched_getaffinity(0))} "
+                      f"capped by the cgroup CPU quota) ({dt:.1f} s)"}
 
 
 if __name__ == "__main__":

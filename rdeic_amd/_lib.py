@@ -46,6 +46,7 @@ class ConvDesc(C.Structure):
         ("out", C.c_void_p), ("out_ld", C.c_int32), ("out_mode", C.c_int32),
         ("dtype", C.c_int32), ("out_f32", C.c_int32),
         ("batch", C.c_int32), ("in_bs", C.c_int64), ("w_bs", C.c_int64), ("out_bs", C.c_int64),
+        ("gn_part", C.c_void_p), ("gn_hw", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -100,6 +101,8 @@ PROTOTYPES = {
     "rdeic_build_gaussian_tables": (C.c_int, [_p, _p, _i32, _i32, _p, _i32, _p, _p]),
     "rdeic_rans_encode": (C.c_int, [_p, _p, _sz, _p, _i32, _p, _p, _i32, _p, _sz, C.POINTER(_sz)]),
     "rdeic_rans_encode_batch": (C.c_int, [_i32, _p, _p, _sz, _sz, _p, _i32, _p, _p, _i32, _p, _sz, _p, _i32]),
+    "rdeic_groupnorm_parts_floats": (C.c_size_t, [_i64, _i32, _i32]),
+    "rdeic_groupnorm_parts_ab": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p]),
     "rdeic_rans_enc_tables_create": (_p, [_p, _i32, _p, _p, _i32]),
     "rdeic_rans_enc_tables_destroy": (None, [_p]),
     "rdeic_rans_encode_batch_t": (C.c_int, [_p, _i32, _p, _p, _sz, _sz, _p, _sz, _p, _i32]),

@@ -53,3 +53,7 @@ static inline int launch_status() {
 }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// GroupNorm statistics of a [rows][c] tensor in the per-row-block partial format of
+// rdeic_groupnorm_parts_ab (norm.hip): the conv launcher's fallback when its epilogue cannot fuse them.
+int gn_rows_partial(const void* x, long rows, int c, int ld, int hw, float* part, int dtype, hipStream_t s);

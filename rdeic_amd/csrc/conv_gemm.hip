@@ -42,6 +42,9 @@ struct ConvArgs {
   int batch;
   int epi_vec;               // 1: LDS-staged vector epilogue where eligible
   int splits, kper;          // split-K: blockIdx.z = split, k-steps [z*kper, (z+1)*kper), raw fp32 partial out
+  float* gn_part;            // fused GroupNorm statistics of the output (see epilogue_vec), or NULL
+  int gn_row0;               // absolute output row of this launch's row 0 (image-group launches)
+  int gn_hw;                 // pixels per image of the GroupNorm those statistics feed
 };
 
 int g_conv_path = 2;  // 0: 128-tiles with the fused GroupNorm prologue only, 2 (default): big-tile auto choice
@@ -111,7 +114,7 @@ __device__ __forceinline__ uint4 gn_apply_chunk(uint4 raw, const float* ab, int 
 // output store are 16-byte coalesced vectors. Same fp32 operation order as the scalar epilogue
 // ((acc + bias) + emb -> act -> + res -> round), so results are bit-identical to it.
 // Needs BM/2 * (BN + 4) * 4 bytes of LDS; the caller has finished with its k-loop buffers.
-__device__ __forceinline__ bool epi_vec_ok(const ConvArgs& a) {
+__host__ __device__ __forceinline__ bool epi_vec_ok(const ConvArgs& a) {
   if (a.out_mode == 2) return (a.cout % 8) == 0 && (a.out_ld % 4) == 0 && ((uintptr_t)a.out % 8) == 0;
   return a.out_mode == 0 && (a.cout % 8) == 0 && (a.out_ld % 8) == 0 && ((uintptr_t)a.out % 16) == 0 &&
          (!a.res || ((a.res_ld % 8) == 0 && ((uintptr_t)a.res % 16) == 0));
@@ -131,6 +134,16 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
   float* L = reinterpret_cast<float*>(lds);
   const int hw_o = a.ho * a.wo;
   const bool of32 = a.out_f32;
+  // Fused GroupNorm statistics (a.gn_part): per output channel and absolute 64-row block, the sum
+  // and the sum of squares of the values as stored (bf16-rounded), in a CANONICAL order that does
+  // not depend on the tile: four 16-row groups, each summed sequentially in row order (fmaf for the
+  // squares), combined as ((g0 + g1) + g2) + g3 — exactly what gn_rows_partial_kernel computes, so
+  // the statistics (and every GroupNorm after them) are identical for every tile and batch size.
+  // Each pass writes its stored values back over its parked accumulators; thread (b, j) then scans
+  // column j of 64-row block b in LDS. Needs WTM in {32, 64} (a wave-row block inside one 64-row
+  // block) and (BM / 64) * BN <= NT; the host enables it only for such tiles (stats_tile_ok).
+  const bool st = a.gn_part != nullptr;
+  float sg[4] = {0.f, 0.f, 0.f, 0.f}, qg[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     __syncthreads();
@@ -195,14 +208,76 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
         float* o = reinterpret_cast<float*>(a.out) + (long)m * a.out_ld + nn;
         *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        if (st) {  // stored values back over the parked accumulators, for the statistics scan
+          *reinterpret_cast<float4*>(L + pr * SDW + cc * 8) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(L + pr * SDW + cc * 8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
       } else {
         bf16 ov[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) ov[e] = from_f32<bf16>(v[e]);
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + nn) = *reinterpret_cast<uint4*>(ov);
+        if (st) {
+          *reinterpret_cast<float4*>(L + pr * SDW + cc * 8) =
+              make_float4(to_f32(ov[0]), to_f32(ov[1]), to_f32(ov[2]), to_f32(ov[3]));
+          *reinterpret_cast<float4*>(L + pr * SDW + cc * 8 + 4) =
+              make_float4(to_f32(ov[4]), to_f32(ov[5]), to_f32(ov[6]), to_f32(ov[7]));
+        }
+      }
+    }
+    if constexpr ((WTM == 32 || WTM == 64) && (BM / 64) * BN <= NT && (WTM / P) % 16 == 0) {
+      if (st) {
+        __syncthreads();
+        const int b = tid / BN, j = tid - (tid / BN) * BN;
+        if (b < BM / 64) {
+          constexpr int WPB = 64 / WTM;  // wave-row blocks per 64-row block
+#pragma unroll
+          for (int w = 0; w < WPB; ++w) {
+            const int wmr = b * WPB + w;
+#pragma unroll
+            for (int k = 0; k < (WTM / P) / 16; ++k) {
+              const int off = w * WTM + p * (WTM / P) + k * 16;  // row offset inside the 64-row block
+              const float* col = L + (wmr * (WTM / P) + k * 16) * SDW + j;
+              const int nv = a.M - (m0 + b * 64 + off);  // valid rows of this 16-row group
+              float s1 = 0.f, s2 = 0.f;
+              if (nv >= 16) {  // all 16 loads issued before the (row-ordered) sums
+                float y[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) y[r] = col[r * SDW];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) { s1 += y[r]; s2 = fmaf(y[r], y[r], s2); }
+              } else {
+                for (int r = 0; r < nv; ++r) { const float y = col[r * SDW]; s1 += y; s2 = fmaf(y, y, s2); }
+              }
+              sg[off >> 4] = s1;
+              qg[off >> 4] = s2;
+            }
+          }
+        }
       }
     }
   }
+  if constexpr ((WTM == 32 || WTM == 64) && (BM / 64) * BN <= NT && (WTM / P) % 16 == 0) {
+    if (st) {
+      const int b = tid / BN, j = tid - (tid / BN) * BN;
+      const int nn = n0 + j;
+      if (b < BM / 64 && nn < a.cout && m0 + b * 64 < a.M) {  // blocks past M are not in the buffer
+        float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0) / 64 + b) * a.cout + nn) * 2;
+        pp[0] = ((sg[0] + sg[1]) + sg[2]) + sg[3];
+        pp[1] = ((qg[0] + qg[1]) + qg[2]) + qg[3];
+      }
+      if (tid == 0 && m0 == 0 && n0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
+    }
+  }
+}
+
+// the compile-time conditions under which epilogue_vec computes fused statistics (mirrors its
+// `if constexpr`): a wave-row block inside one 64-row block, 16-row groups per pass, one thread per
+// (64-row block, channel)
+template <int BM, int BN, int WGM, int NT, int P>
+constexpr bool stats_tile_ok() {
+  constexpr int WTM = BM / WGM;
+  return (WTM == 32 || WTM == 64) && (WTM / P) % 16 == 0 && (BM / 64) * BN <= NT;
 }
 
 // GNP: compile the GroupNorm+SiLU gather prologue in (false = plain gather, fewer VGPRs / VALU).
@@ -512,7 +587,16 @@ int launch_cfg(const ConvArgs& a, bool vec, hipStream_t s) {
 
 // register-staged, no GN prologue (bf16, 16-byte gathers): the big-tile main path
 template <int BM, int BN, int WGM, int WGN>
-int launch_plain(const ConvArgs& a, hipStream_t s) {
+int launch_plain(ConvArgs a, hipStream_t s, bool* fused) {
+  if (a.gn_part) {  // statistics in conv_kernel's vector epilogue (P = 2) where the tile allows
+    constexpr int TM = BM / WGM / 16;
+    constexpr bool swz = WGM * WGN <= 8;
+    constexpr bool fits = TM % 2 == 0 && (BM / 2) * (BN + 4) * 4 <= conv_lds_bytes<bf16, BM, BN, swz>();
+    const bool ok = fits && stats_tile_ok<BM, BN, WGM, WGM * WGN * 64, 2>() && g_swz && a.epi_vec && epi_vec_ok(a) &&
+                    a.gn_hw > 0 && a.gn_hw % 64 == 0 && a.batch == 1 && a.splits <= 1 && a.out_mode == 0;
+    if (!ok) a.gn_part = nullptr;
+    if (fused) *fused = ok;
+  }
   dim3 grid(cdiv(a.M, BM), cdiv(a.cout, BN), a.batch);
   // measured A/B (one process, bit-identical results): the swizzled 128-B rows win on the
   // 4- and 8-wave tiles (+3-6 %) and lose on the 16-wave 256x256 tile (-16 %), which keeps the
@@ -537,7 +621,7 @@ int launch_plain(const ConvArgs& a, hipStream_t s) {
 
 // Tile choice for the plain path: maximise (useful fraction of the padded tile grid) x (CU fill)
 // x (operand reuse of the tile); the accumulation order does not depend on the choice.
-int launch_plain_auto(const ConvArgs& a, hipStream_t s, int tile = -1) {
+int launch_plain_auto(const ConvArgs& a, hipStream_t s, int tile = -1, bool* fused = nullptr) {
   struct Cand { int bm, bn; float reuse; };
   const Cand cands[] = {{256, 256, 1.0f}, {256, 128, 0.86f}, {128, 256, 0.86f}, {128, 128, 0.72f}, {64, 128, 0.55f},
                         {128, 64, 0.55f}};
@@ -554,17 +638,17 @@ int launch_plain_auto(const ConvArgs& a, hipStream_t s, int tile = -1) {
   if (g_force_tile >= 0 && g_force_tile < 11) best = g_force_tile;
   if (tile >= 0 && tile < 11 && tile != 5) best = tile;
   switch (best) {
-    case 0: return launch_plain<256, 256, 4, 4>(a, s);
-    case 1: return launch_plain<256, 128, 4, 2>(a, s);
-    case 2: return launch_plain<128, 256, 2, 4>(a, s);
-    case 3: return launch_plain<128, 128, 2, 2>(a, s);
-    case 4: return launch_plain<64, 128, 2, 2>(a, s);
-    case 6: return launch_plain<256, 128, 4, 4>(a, s);
-    case 7: return launch_plain<128, 256, 4, 4>(a, s);
-    case 8: return launch_plain<128, 128, 2, 4>(a, s);
-    case 9: return launch_plain<128, 128, 4, 4>(a, s);
-    case 10: return launch_plain<64, 128, 2, 4>(a, s);
-    default: return launch_plain<128, 64, 2, 2>(a, s);
+    case 0: return launch_plain<256, 256, 4, 4>(a, s, fused);
+    case 1: return launch_plain<256, 128, 4, 2>(a, s, fused);
+    case 2: return launch_plain<128, 256, 2, 4>(a, s, fused);
+    case 3: return launch_plain<128, 128, 2, 2>(a, s, fused);
+    case 4: return launch_plain<64, 128, 2, 2>(a, s, fused);
+    case 6: return launch_plain<256, 128, 4, 4>(a, s, fused);
+    case 7: return launch_plain<128, 256, 4, 4>(a, s, fused);
+    case 8: return launch_plain<128, 128, 2, 4>(a, s, fused);
+    case 9: return launch_plain<128, 128, 4, 4>(a, s, fused);
+    case 10: return launch_plain<64, 128, 2, 4>(a, s, fused);
+    default: return launch_plain<128, 64, 2, 2>(a, s, fused);
   }
 }
 
@@ -960,8 +1044,25 @@ bool dma_ok(const rdeic_conv_desc* d, const ConvArgs& a, unsigned& b0, unsigned&
   return true;
 }
 
+// Whether the kernel's vector epilogue runs for these arguments (the compile-time part mirrors the
+// `if constexpr` in conv_dma_kernel).
 template <int BM, int BN, int WGM, int WGN, int S, int EP>
-int launch_dma(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s) {
+bool dma_vec_epilogue(const ConvArgs& a) {
+  constexpr int TM = BM / WGM / 16;
+  constexpr bool fits = TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * (BM + BN) * 128;
+  return fits && (a.epi_vec || a.out_mode == 2) && epi_vec_ok(a);
+}
+
+// gn_hw: pixels per image of the GroupNorm the statistics feed; the 64-row partial blocks must not
+// straddle two images, and the epilogue must be the vector one with a statistics-capable tile.
+template <int BM, int BN, int WGM, int WGN, int S, int EP>
+int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int gn_hw, bool* fused) {
+  if (a.gn_part) {
+    const bool ok = a.splits <= 1 && a.batch == 1 && a.out_mode == 0 && gn_hw > 0 && gn_hw % 64 == 0 &&
+                    stats_tile_ok<BM, BN, WGM, WGM * WGN * 64, EP>() && dma_vec_epilogue<BM, BN, WGM, WGN, S, EP>(a);
+    if (!ok) a.gn_part = nullptr;
+    if (fused) *fused = ok;
+  }
   const int tn = cdiv(a.cout, BN);
   const long tiles = (long)cdiv(a.M, BM) * tn;
   dim3 grid((unsigned)tiles, 1, a.splits > 1 ? a.splits : a.batch);
@@ -978,7 +1079,8 @@ int launch_dma(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hipStre
 // without padding waste (1.19-1.27 PF on the VAE 512-channel layers), 25 on the rest with >= 256
 // 128x128 tiles, the 4-wave 64x128 tile when even that grid cannot fill the chip; 34 often wins
 // on short-K linears (the autotuner in rdeic_amd/ops.py picks per shape).
-int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int tile) {
+int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int tile,
+                    int gn_hw = 0, bool* fused = nullptr) {
   if (tile < 20 || tile > 34) {
     const long zb = a.splits > 1 ? a.splits : a.batch;
     const long t128 = (long)cdiv(a.M, 128) * cdiv(a.cout, 128) * zb;
@@ -987,21 +1089,21 @@ int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hi
     tile = (t256 >= 256 && useful256 >= 0.9f) ? 32 : t128 >= 256 ? 25 : 26;
   }
   switch (tile) {
-    case 20: return launch_dma<256, 256, 2, 4, 2, 4>(a, b0, b1, bw, s);
-    case 21: return launch_dma<256, 128, 4, 2, 3, 2>(a, b0, b1, bw, s);
-    case 22: return launch_dma<128, 256, 2, 4, 3, 2>(a, b0, b1, bw, s);
-    case 24: return launch_dma<128, 128, 2, 2, 2, 2>(a, b0, b1, bw, s);
-    case 25: return launch_dma<128, 128, 2, 4, 2, 2>(a, b0, b1, bw, s);
-    case 26: return launch_dma<64, 128, 2, 2, 3, 2>(a, b0, b1, bw, s);
-    case 27: return launch_dma<128, 128, 2, 4, 3, 2>(a, b0, b1, bw, s);
-    case 28: return launch_dma<256, 128, 4, 2, 2, 2>(a, b0, b1, bw, s);
-    case 29: return launch_dma<128, 256, 2, 4, 2, 2>(a, b0, b1, bw, s);
-    case 30: return launch_dma<64, 128, 2, 2, 2, 2>(a, b0, b1, bw, s);
-    case 31: return launch_dma<128, 64, 2, 2, 2, 2>(a, b0, b1, bw, s);
-    case 32: return launch_dma<256, 256, 4, 4, 2, 4>(a, b0, b1, bw, s);
-    case 33: return launch_dma<256, 128, 4, 4, 2, 2>(a, b0, b1, bw, s);
-    case 34: return launch_dma<128, 128, 4, 4, 2, 2>(a, b0, b1, bw, s);
-    default: return launch_dma<128, 128, 2, 2, 3, 2>(a, b0, b1, bw, s);
+    case 20: return launch_dma<256, 256, 2, 4, 2, 4>(a, b0, b1, bw, s, gn_hw, fused);
+    case 21: return launch_dma<256, 128, 4, 2, 3, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 22: return launch_dma<128, 256, 2, 4, 3, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 24: return launch_dma<128, 128, 2, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 25: return launch_dma<128, 128, 2, 4, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 26: return launch_dma<64, 128, 2, 2, 3, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 27: return launch_dma<128, 128, 2, 4, 3, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 28: return launch_dma<256, 128, 4, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 29: return launch_dma<128, 256, 2, 4, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 30: return launch_dma<64, 128, 2, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 31: return launch_dma<128, 64, 2, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 32: return launch_dma<256, 256, 4, 4, 2, 4>(a, b0, b1, bw, s, gn_hw, fused);
+    case 33: return launch_dma<256, 128, 4, 4, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 34: return launch_dma<128, 128, 4, 4, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    default: return launch_dma<128, 128, 2, 2, 3, 2>(a, b0, b1, bw, s, gn_hw, fused);
   }
 }
 
@@ -1010,7 +1112,7 @@ int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec);
 // Images are independent in a conv, so a launch whose buffers exceed the 2 GiB reach of a
 // 32-bit buffer offset runs the DMA kernel over groups of images (same per-pixel arithmetic,
 // bit-identical). Returns -1 when the DMA path does not apply.
-int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipStream_t s) {
+int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipStream_t s, bool* fused = nullptr) {
   ConvArgs a;
   bool vec = false;
   if (make_args(d, a, vec) != RDEIC_OK || !vec) return -1;
@@ -1020,8 +1122,9 @@ int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipSt
       a.splits = splits; a.kper = (a.nk + splits - 1) / splits;
       a.bias = nullptr; a.emb = nullptr; a.act = 0; a.res = nullptr;
       a.out = (char*)ws; a.out_ld = a.cout; a.out_f32 = 1; a.out_mode = 0;
+      a.gn_part = nullptr;
     }
-    return launch_dma_auto(a, b0, b1, bw, s, tile);
+    return launch_dma_auto(a, b0, b1, bw, s, tile, d->gn_hw, fused);
   }
   if (splits > 1 || d->batch > 1 || d->n <= 1) return -1;
   // per-image sizes (bytes); pick the largest image group that fits
@@ -1042,10 +1145,13 @@ int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipSt
     e.emb = d->emb ? d->emb + (long)i0 * d->emb_ld : nullptr;
     ConvArgs ea;
     if (make_args(&e, ea, vec) != RDEIC_OK || !vec || !dma_ok(&e, ea, b0, b1, bw)) return -1;
-    const int rc = launch_dma_auto(ea, b0, b1, bw, s, tile);
+    ea.gn_row0 = i0 * d->ho * d->wo;
+    bool f = false;
+    const int rc = launch_dma_auto(ea, b0, b1, bw, s, tile, d->gn_hw, &f);
     if (rc != RDEIC_OK) return rc;
+    if (fused) *fused = (i0 == 0 ? f : (*fused && f));
   }
-  return RDEIC_OK;
+  return RDEIC_OK;  // *fused false if any group could not fuse: the caller recomputes the statistics
 }
 
 }  // namespace
@@ -1072,6 +1178,7 @@ int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec) {
   a.out_f32 = d->out_f32;
   a.epi_vec = g_epi_vec;
   a.splits = 1; a.kper = 0;
+  a.gn_part = d->gn_part; a.gn_row0 = 0; a.gn_hw = d->gn_hw;
   a.M = d->n * d->ho * d->wo;
   a.batch = d->batch > 1 ? d->batch : 1;
   a.in_bs = d->in_bs; a.w_bs = d->w_bs; a.out_bs = d->out_bs;
@@ -1094,11 +1201,13 @@ int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec) {
 }
 }  // namespace
 
-static int conv2d_impl(const rdeic_conv_desc* d, void* stream) {
+static int conv2d_run(const rdeic_conv_desc* d, void* stream, bool* fused) {
   ConvArgs a;
   bool vec = false;
   const int rc = make_args(d, a, vec);
   if (rc != RDEIC_OK) return rc;
+  float* const part = a.gn_part;
+  a.gn_part = nullptr;  // statistics fuse into the LDS-DMA (dma_grouped reads d) and big-tile register paths
   hipStream_t s = (hipStream_t)stream;
   if (d->out_mode == 2) {  // fused GEGLU exists in the LDS-DMA kernel's vector epilogue only
     const int rc2 = vec ? dma_grouped(d, -1, 1, nullptr, s) : -1;
@@ -1111,10 +1220,11 @@ static int conv2d_impl(const rdeic_conv_desc* d, void* stream) {
     return launch_smallc(a, s);
   if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path != 0) {
     if (g_dma) {
-      const int rc2 = dma_grouped(d, -1, 1, nullptr, s);
+      const int rc2 = dma_grouped(d, -1, 1, nullptr, s, fused);
       if (rc2 != -1) return rc2;
     }
-    return launch_plain_auto(a, s);
+    a.gn_part = part;
+    return launch_plain_auto(a, s, -1, fused);
   }
   if (d->dtype == 1) {
     if (d->cout <= 16) return launch_cfg<bf16, 128, 16, 4, 1>(a, vec, s);
@@ -1131,7 +1241,7 @@ static int conv2d_impl(const rdeic_conv_desc* d, void* stream) {
 // Explicit tile choice for the big-tile path (autotuning by the caller; every tile gives
 // bit-identical results). tile -1 = the built-in heuristic. Shapes outside the big-tile path
 // (GN prologue, cout <= 32, fp32, unaligned) ignore it and run exactly as rdeic_conv2d.
-static int conv2d_tile_impl(const rdeic_conv_desc* d, int32_t tile, void* stream) {
+static int conv2d_tile_run(const rdeic_conv_desc* d, int32_t tile, void* stream, bool* fused) {
   ConvArgs a;
   bool vec = false;
   const int rc = make_args(d, a, vec);
@@ -1142,13 +1252,37 @@ static int conv2d_tile_impl(const rdeic_conv_desc* d, int32_t tile, void* stream
   }
   if (d->dtype == 1 && vec && !d->gn_ab && d->cout > 32 && g_conv_path != 0) {
     if (tile >= 20) {
-      const int rc2 = dma_grouped(d, tile, 1, nullptr, (hipStream_t)stream);
+      const int rc2 = dma_grouped(d, tile, 1, nullptr, (hipStream_t)stream, fused);
       if (rc2 != -1) return rc2;
       tile = -1;
     }
-    return launch_plain_auto(a, (hipStream_t)stream, tile);
+    return launch_plain_auto(a, (hipStream_t)stream, tile, fused);
   }
-  return conv2d_impl(d, stream);
+  return conv2d_run(d, stream, fused);
+}
+
+static double conv_flops(const rdeic_conv_desc* d) {
+  if (!d) return 0.0;
+  const double b = d->batch > 1 ? d->batch : 1;
+  return 2.0 * b * d->n * d->ho * d->wo * d->cout * (double)d->kh * d->kw * (d->c0 + d->c1);
+}
+
+// d->gn_part: the output's GroupNorm statistics in the partial format of rdeic_groupnorm_parts_ab,
+// fused into the epilogue where the launch allows it, else by a separate pass over the output.
+static int conv2d_impl(const rdeic_conv_desc* d, int32_t tile, void* stream) {
+  if (d && d->gn_part &&
+      (d->gn_hw <= 0 || d->gn_hw % 64 || d->batch > 1 || d->out_mode != 0 || (long)d->n * d->ho * d->wo % d->gn_hw))
+    return RDEIC_EINVAL;
+  bool fused = false;
+  int rc;
+  {
+    ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
+    rc = tile == -2 ? conv2d_run(d, stream, &fused) : conv2d_tile_run(d, tile, stream, &fused);
+  }
+  if (rc != RDEIC_OK || !d->gn_part || fused) return rc;
+  const long rows = (long)d->n * d->ho * d->wo;
+  return gn_rows_partial(d->out, rows, d->cout, d->out_ld, d->gn_hw, d->gn_part,
+                         (d->out_f32 || d->dtype == 0) ? 0 : 1, (hipStream_t)stream);
 }
 
 // Split-K variant (small-M, large-K layers): `splits` k-ranges computed into a caller-provided
@@ -1175,7 +1309,7 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
     return launch_status();
   }
   ConvArgs p = a;  // partial pass: raw sums into the workspace
-  p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr;
+  p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr;
   p.out = (char*)ws; p.out_ld = a.cout; p.out_f32 = 1;
   p.splits = splits;
   p.kper = (a.nk + splits - 1) / splits;
@@ -1190,26 +1324,25 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
 }
 
 // algorithmic FLOPs of one launch (2 per MAC), for the launch profiler
-static double conv_flops(const rdeic_conv_desc* d) {
-  if (!d) return 0.0;
-  const double b = d->batch > 1 ? d->batch : 1;
-  return 2.0 * b * d->n * d->ho * d->wo * d->cout * (double)d->kh * d->kw * (d->c0 + d->c1);
-}
 
-extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) {
-  ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
-  return conv2d_impl(d, stream);
-}
+extern "C" int rdeic_conv2d(const rdeic_conv_desc* d, void* stream) { return conv2d_impl(d, -2, stream); }
 
 extern "C" int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream) {
-  ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
-  return conv2d_tile_impl(d, tile, stream);
+  return conv2d_impl(d, tile, stream);
 }
 
 extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats,
                                    void* stream) {
-  ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
-  return conv2d_splitk_impl(d, splits, ws, ws_floats, stream);
+  if (d && d->gn_part && (d->gn_hw <= 0 || d->gn_hw % 64 || (long)d->n * d->ho * d->wo % d->gn_hw))
+    return RDEIC_EINVAL;
+  int rc;
+  {
+    ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
+    rc = conv2d_splitk_impl(d, splits, ws, ws_floats, stream);
+  }
+  if (rc != RDEIC_OK || !d->gn_part) return rc;  // statistics of the reduced output: stand-alone pass
+  return gn_rows_partial(d->out, (long)d->n * d->ho * d->wo, d->cout, d->out_ld, d->gn_hw, d->gn_part,
+                         d->out_f32 ? 0 : 1, (hipStream_t)stream);
 }
 
 extern "C" int rdeic_set_conv_path(int32_t path) {

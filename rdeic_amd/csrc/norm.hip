@@ -385,7 +385,127 @@ int gn_stats(const void* x0, int32_t c0, int32_t ld0, const void* x1, int32_t c1
   return launch_status();
 }
 
+// ---- GroupNorm from per-row-block partial sums (the conv epilogue's fused statistics) ----------
+// Partial format: a 16-byte header whose first int32 is R = 64 (rows per partial), then
+// [rows / 64][c][2] fp32 (sum, sum of squares) of the tensor's stored values over each 64-row
+// block, in the canonical order ((g0 + g1) + g2) + g3 of four 16-row groups summed sequentially
+// (fmaf for the squares). The conv epilogue writes the same numbers (conv_gemm.hip, epilogue_vec);
+// this kernel is its stand-alone fallback. 64 divides the image's pixel count (no straddling).
+template <typename T>
+__global__ __launch_bounds__(256) void gn_rows_partial_kernel(const T* __restrict__ x, long rows, int c, int ld,
+                                                              float* __restrict__ part) {
+  const int blk = blockIdx.x, ch = blockIdx.y * 256 + threadIdx.x;
+  if (blk == 0 && ch == 0) reinterpret_cast<int*>(part)[0] = 64;
+  if (ch >= c) return;
+  const T* xp = x + (long)blk * 64 * ld + ch;
+  float sg[4], qg[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const long nv = rows - ((long)blk * 64 + g * 16);  // valid rows of this 16-row group
+    float s1 = 0.f, s2 = 0.f;
+    if (nv >= 16) {  // 16 loads in flight, then the row-ordered sums
+      float y[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) y[r] = to_f32(xp[(long)(g * 16 + r) * ld]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s1 += y[r]; s2 = fmaf(y[r], y[r], s2); }
+    } else {
+      for (int r = 0; r < nv; ++r) {
+        const float v = to_f32(xp[(long)(g * 16 + r) * ld]);
+        s1 += v;
+        s2 = fmaf(v, v, s2);
+      }
+    }
+    sg[g] = s1;
+    qg[g] = s2;
+  }
+  float* o = part + 4 + ((long)blk * c + ch) * 2;
+  o[0] = ((sg[0] + sg[1]) + sg[2]) + sg[3];
+  o[1] = ((qg[0] + qg[1]) + qg[2]) + qg[3];
+}
+
+__device__ __forceinline__ double block_sum256_d(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// One 256-thread block per (group, image). Channels [0, c0) come from p0, [c0, c0 + c1) from p1
+// (the UNet's skip concat); sums in fp64 in a fixed order (deterministic); var = E[x^2] - mean^2.
+__global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const float* __restrict__ p0, int c0,
+                                                                const float* __restrict__ p1, int c1, int hw,
+                                                                int groups, float eps, const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta,
+                                                                float* __restrict__ ab) {
+  const int img = blockIdx.y, g = blockIdx.x, t = threadIdx.x;
+  const int c = c0 + c1, cpg = c / groups, ga = g * cpg, gb = ga + cpg;
+  __shared__ double red[4];
+  double S = 0.0, Q = 0.0;
+  for (int sgi = 0; sgi < 2; ++sgi) {
+    const float* p = sgi ? p1 : p0;
+    const int base = sgi ? c0 : 0, cs = sgi ? c1 : c0;
+    const int lo = max(ga, base), hi = min(gb, base + cs);
+    if (hi <= lo) continue;
+    const int R = reinterpret_cast<const int*>(p)[0];
+    const int T = hw / R, nch = hi - lo;
+    const float* q = p + 4 + ((long)img * T * cs + (lo - base)) * 2;
+    for (int i = t; i < T * nch; i += 256) {
+      const int tt = i / nch, j = i - tt * nch;
+      const float* e = q + ((long)tt * cs + j) * 2;
+      S += (double)e[0];
+      Q += (double)e[1];
+    }
+  }
+  S = block_sum256_d(S, red);
+  Q = block_sum256_d(Q, red);
+  const double N = (double)hw * cpg;
+  const double mean = S / N;
+  const float var = (float)fmax(Q / N - mean * mean, 0.0);
+  const float rstd = rsqrtf(var + eps);
+  const float mf = (float)mean;
+  for (int j = t; j < cpg; j += 256) {
+    const int ch = ga + j;
+    const float gm = gamma ? gamma[ch] : 1.f, be = beta ? beta[ch] : 0.f;
+    const float av = gm * rstd;
+    ab[((long)img * c + ch) * 2 + 0] = av;
+    ab[((long)img * c + ch) * 2 + 1] = be - mf * av;
+  }
+}
+
 }  // namespace
+
+// stand-alone partials of a [rows][c] (pixel stride ld) tensor (declared in common.h for the conv
+// launcher's fallback); hw (pixels per image) must be a multiple of 64
+int gn_rows_partial(const void* x, long rows, int c, int ld, int hw, float* part, int dtype, hipStream_t s) {
+  if (hw % 64 || rows % hw) return RDEIC_EINVAL;
+  dim3 grid((unsigned)(rows / 64), (unsigned)((c + 255) / 256));
+  if (dtype == 1)
+    hipLaunchKernelGGL(gn_rows_partial_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, rows, c, ld, part);
+  else
+    hipLaunchKernelGGL(gn_rows_partial_kernel<float>, grid, dim3(256), 0, s, (const float*)x, rows, c, ld, part);
+  return launch_status();
+}
+
+extern "C" size_t rdeic_groupnorm_parts_floats(int64_t rows, int32_t c, int32_t hw) {
+  if (hw <= 0 || hw % 64 || rows <= 0 || c <= 0) return 0;  // 0: statistics cannot be fused for this shape
+  return (size_t)(4 + (rows / 64) * c * 2);
+}
+
+extern "C" int rdeic_groupnorm_parts_ab(const float* p0, int32_t c0, const float* p1, int32_t c1, int32_t n,
+                                        int32_t hw, int32_t groups, float eps, const float* gamma, const float* beta,
+                                        float* ab, void* stream) {
+  const int c = c0 + c1;
+  if (!p0 || !ab || n <= 0 || hw <= 0 || hw % 64 || c0 <= 0 || c1 < 0 || (c1 > 0 && !p1) || groups <= 0 ||
+      c % groups)
+    return RDEIC_EINVAL;
+  hipLaunchKernelGGL(gn_finalize_parts_kernel, dim3(groups, n), dim3(256), 0, (hipStream_t)stream, p0, c0,
+                     p1 ? p1 : p0, c1, hw, groups, eps, gamma, beta, ab);
+  return launch_status();
+}
 
 extern "C" size_t rdeic_groupnorm_ws_floats(int32_t n, int32_t hw, int32_t c) {
   const int pix_per = gn_chunk(hw, 2);  // the bf16 chunk is never larger than the fp32 one

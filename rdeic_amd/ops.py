@@ -89,9 +89,12 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
            gn: Optional[torch.Tensor] = None, gn_silu: bool = False, emb: Optional[torch.Tensor] = None,
            act: int = NONE, slope: float = 0.0, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False,
-           geglu: bool = False) -> torch.Tensor:
+           geglu: bool = False, stats: bool = False, stats_hw: Optional[int] = None) -> torch.Tensor:
     """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC).
-    geglu: p packed by ParamStore.conv_geglu; out = value * gelu(gate), cout/2 channels (bf16)."""
+    geglu: p packed by ParamStore.conv_geglu; out = value * gelu(gate), cout/2 channels (bf16).
+    stats: the output feeds a GroupNorm — its statistics are produced with it (fused into the conv
+    epilogue where the tile allows, rdeic_conv_desc.gn_part) and group_norm_ab(out) then needs no
+    pass over the tensor. stats_hw: pixels per image of that GroupNorm (default ho*wo)."""
     if gn is not None and _gn_materialize(x, x2, p):
         # the big-tile conv path has no GroupNorm prologue (it is VALU-bound there): materialise the
         # normalised (concatenated) input once with the vectorised, HBM-rate apply kernel instead
@@ -165,6 +168,13 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     d.dtype = dt_code(x)
     d.out_f32 = int(odt == torch.float32 and x.dtype != torch.float32)
     d.batch = 1
+    part = None
+    if stats and GN_STATS_FUSE and x.dtype == torch.bfloat16 and not (geglu or pixel_shuffle):
+        ghw = int(stats_hw or ho * wo)
+        nf = int(_lib.load().rdeic_groupnorm_parts_floats(n * ho * wo, p.cout, ghw))
+        if nf:  # 0: the image size is not a multiple of 64 pixels; the GroupNorm reads the tensor
+            part = torch.empty(nf, dtype=torch.float32, device=x.device)
+            d.gn_part, d.gn_hw = part.data_ptr(), ghw
     flops = 2.0 * n * ho * wo * p.cout * p.kh * p.kw * p.cin
     splits = _splitk_count(x, x2, n * ho * wo, p, gn is not None or pixel_shuffle or geglu, out)
 
@@ -188,7 +198,29 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
         _launch(tag, "rdeic_conv2d_tile", C.byref(d), tile, stream_ptr())
     else:
         _launch(tag, "rdeic_conv2d", C.byref(d), stream_ptr())
+    if part is not None:
+        _attach_gn_part(out, part, d.gn_hw)
     return out
+
+
+# Fused GroupNorm statistics (conv2d(stats=True) -> group_norm_ab): the partial sums travel as an
+# attribute of the output tensor object, keyed on its storage and shape, so a view or a different
+# tensor never picks up another tensor's statistics (it simply takes the stand-alone stats pass).
+GN_STATS_FUSE = True
+
+
+def _attach_gn_part(t: torch.Tensor, part: torch.Tensor, hw: int) -> None:
+    t._rdeic_gn_part = (part, t.data_ptr(), tuple(t.shape), tuple(t.stride()), hw)
+
+
+def _gn_part_of(t: Optional[torch.Tensor], hw: int):
+    info = getattr(t, "_rdeic_gn_part", None) if t is not None else None
+    if info is None:
+        return None
+    part, ptr, shape, stride, phw = info
+    if ptr != t.data_ptr() or shape != tuple(t.shape) or stride != tuple(t.stride()) or phw != hw:
+        return None
+    return part
 
 
 # Tile choice for the big-tile bf16 conv path. Every tile produces bit-identical results (same BK,
@@ -410,9 +442,12 @@ def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) 
 
 
 def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, out_f32: bool = False, geglu: bool = False) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, out_f32: bool = False, geglu: bool = False,
+           stats_hw: Optional[int] = None) -> torch.Tensor:
     """Token-wise Linear over a [rows, c] tensor (1x1 conv over a rows x 1 image).
-    geglu: fused GEGLU projection (p from ParamStore.conv_geglu), output [rows, cout/2]."""
+    geglu: fused GEGLU projection (p from ParamStore.conv_geglu), output [rows, cout/2].
+    stats_hw: the output (as [rows/stats_hw images, stats_hw tokens]) feeds a GroupNorm; its
+    statistics are produced with it (conv2d(stats=True)); reshape with ops.tokens_to_nhwc."""
     rows, c = x.shape
     x4 = x.as_strided((1, rows, 1, c), (rows * x.stride(0), x.stride(0), x.stride(0), 1))
     odt = torch.float32 if (out_f32 or x.dtype == torch.float32) else x.dtype
@@ -423,8 +458,21 @@ def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[tor
     r4 = None
     if res is not None:
         r4 = res.as_strided((1, rows, 1, p.cout), (rows * res.stride(0), res.stride(0), res.stride(0), 1))
-    conv2d(x4, p, act=act, res=r4, out=o4, out_f32=out_f32, geglu=geglu)
+    conv2d(x4, p, act=act, res=r4, out=o4, out_f32=out_f32, geglu=geglu, stats=stats_hw is not None,
+           stats_hw=stats_hw)
+    info = getattr(o4, "_rdeic_gn_part", None)
+    if info is not None:
+        out._rdeic_gn_tokens = info  # carried to the NHWC view by tokens_to_nhwc
     return out
+
+
+def tokens_to_nhwc(t: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    """[n*h*w, c] token rows -> NHWC view, keeping fused GroupNorm statistics of linear(stats_hw=h*w)."""
+    v = t.view(n, h, w, t.shape[1])
+    info = getattr(t, "_rdeic_gn_tokens", None)
+    if info is not None and info[4] == h * w:
+        _attach_gn_part(v, info[0], h * w)
+    return v
 
 
 def gemm_batched(a: torch.Tensor, b_nk: torch.Tensor, out: torch.Tensor, *, batch: int, m: int, n: int, k: int,
@@ -455,6 +503,13 @@ def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, grou
     ld0 = pix_ld(x)
     c1, ld1 = (x2.shape[3], pix_ld(x2)) if x2 is not None else (0, 0)
     c = c0 + c1
+    p0, p1 = _gn_part_of(x, h * w), _gn_part_of(x2, h * w)
+    if p0 is not None and (x2 is None or p1 is not None):
+        # statistics came with the producing conv: only the per-(image, group) finalize runs
+        ab = torch.empty((n, c, 2), dtype=torch.float32, device=x.device)
+        call("rdeic_groupnorm_parts_ab", p0.data_ptr(), c0, _ptr(p1), c1, n, h * w, groups, float(eps),
+             gamma.data_ptr(), beta.data_ptr(), ab.data_ptr(), stream_ptr())
+        return ab
     ws = torch.empty(int(_lib.load().rdeic_groupnorm_ws_floats(n, h * w, c)), dtype=torch.float32, device=x.device)
     ab = torch.empty((n, c, 2), dtype=torch.float32, device=x.device)
     _launch(("gn_stats", float(n * h * w * c * x.element_size()), None),

@@ -193,12 +193,13 @@ class UNet:
         return ops.linear(e, stacked)
 
     def resblock(self, rb: ResBlock, x: torch.Tensor, emb_all: torch.Tensor,
-                 x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 x2: Optional[torch.Tensor] = None, stats: bool = False) -> torch.Tensor:
+        """stats: the output feeds a GroupNorm (its statistics come fused with the last conv)."""
         s = self.store
         ab1 = ops.group_norm_ab(x, s.get(rb.prefix + ".in_layers.0.weight"), s.get(rb.prefix + ".in_layers.0.bias"),
                                 rb.gn_in, 1e-5, x2=x2)
         h = ops.conv2d(x, s.conv(rb.prefix + ".in_layers.2"), x2=x2, gn=ab1, gn_silu=True,
-                       emb=emb_all[:, rb.emb_off:rb.emb_off + rb.cout])
+                       emb=emb_all[:, rb.emb_off:rb.emb_off + rb.cout], stats=True)
         ab2 = ops.group_norm_ab(h, s.get(rb.prefix + ".out_layers.0.weight"),
                                 s.get(rb.prefix + ".out_layers.0.bias"), rb.gn_out, 1e-5)
         if rb.cin != rb.cout:
@@ -207,10 +208,10 @@ class UNet:
             if x2 is not None:
                 raise ValueError("identity skip with a concatenated input")
             skip = x
-        return ops.conv2d(h, s.conv(rb.prefix + ".out_layers.3"), gn=ab2, gn_silu=True, res=skip)
+        return ops.conv2d(h, s.conv(rb.prefix + ".out_layers.3"), gn=ab2, gn_silu=True, res=skip, stats=stats)
 
     def transformer(self, t: SpatialTransformer, x: torch.Tensor, ctx_kv_in: torch.Tensor, ctx_batch: int,
-                    ctx_len: int) -> torch.Tensor:
+                    ctx_len: int, stats: bool = False) -> torch.Tensor:
         s = self.store
         B, H, W_, C = x.shape
         L = H * W_
@@ -244,24 +245,27 @@ class UNet:
         # proj_out + residual to the block input
         if not x.is_contiguous():
             raise ValueError("transformer input must be contiguous NHWC")
-        out = ops.linear(h, s.conv(t.prefix + ".proj_out"), res=x.view(rows, C))
-        return out.view(B, H, W_, C)
+        out = ops.linear(h, s.conv(t.prefix + ".proj_out"), res=x.view(rows, C), stats_hw=L if stats else None)
+        return ops.tokens_to_nhwc(out, B, H, W_)
 
-    def run_layers(self, layers, x, emb_all, ctx_rows, ctx_batch, ctx_len, x2=None):
+    def run_layers(self, layers, x, emb_all, ctx_rows, ctx_batch, ctx_len, x2=None, stats_last: bool = True):
+        """Every layer's output but the last feeds the next layer's GroupNorm, so it carries fused
+        statistics; the last one does when stats_last (its consumer is a GroupNorm too)."""
         s = self.store
-        for layer in layers:
+        for li, layer in enumerate(layers):
+            st = stats_last or li + 1 < len(layers)
             if isinstance(layer, Conv):
-                x = ops.conv2d(x, s.conv(layer.prefix), x2=x2)
+                x = ops.conv2d(x, s.conv(layer.prefix), x2=x2, stats=st)
                 x2 = None
             elif isinstance(layer, ResBlock):
-                x = self.resblock(layer, x, emb_all, x2=x2)
+                x = self.resblock(layer, x, emb_all, x2=x2, stats=st)
                 x2 = None
             elif isinstance(layer, SpatialTransformer):
-                x = self.transformer(layer, x, ctx_rows, ctx_batch, ctx_len)
+                x = self.transformer(layer, x, ctx_rows, ctx_batch, ctx_len, stats=st)
             elif isinstance(layer, Down):
-                x = ops.conv2d(x, s.conv(layer.prefix, stride=2, pad=1))
+                x = ops.conv2d(x, s.conv(layer.prefix, stride=2, pad=1), stats=st)
             elif isinstance(layer, Up):
-                x = ops.conv2d(x, s.conv(layer.prefix), up2=True)
+                x = ops.conv2d(x, s.conv(layer.prefix), up2=True, stats=st)
             else:
                 raise TypeError(layer)
         return x
@@ -350,19 +354,24 @@ class NoiseEstimator:
         h_base = ops.cast(x, dt)
         h_ctr, ctr_x2 = h_base, hint
         hs_base, hs_ctr = [], []
+        # GroupNorm statistics travel with the tensors the GroupNorms read: the base features after
+        # each zero-conv add (next block, and the decoder's skip concat), the control features, the
+        # last decoder block's output (the final norm)
         for i, (lb, lc) in enumerate(zip(self.base.input_blocks, self.ctrl.input_blocks)):
-            h_base = self.base.run_layers(lb, h_base, emb_b, ctx_rows, Bc, Lc)
+            h_base = self.base.run_layers(lb, h_base, emb_b, ctx_rows, Bc, Lc, stats_last=False)
             h_ctr = self.ctrl.run_layers(lc, h_ctr, emb_c, ctx_rows, Bc, Lc, x2=ctr_x2)
             ctr_x2 = None
-            h_base = ops.conv2d(h_ctr, s.conv(self.enc_zero[i], scale=sc), res=h_base)
+            h_base = ops.conv2d(h_ctr, s.conv(self.enc_zero[i], scale=sc), res=h_base, stats=True)
             hs_base.append(h_base)
             hs_ctr.append(h_ctr)
-        h_base = self.base.run_layers(self.base.middle, h_base, emb_b, ctx_rows, Bc, Lc)
-        h_ctr = self.ctrl.run_layers(self.ctrl.middle, h_ctr, emb_c, ctx_rows, Bc, Lc)
-        h_base = ops.conv2d(h_ctr, s.conv(self.mid_zero, scale=sc), res=h_base)
+        h_base = self.base.run_layers(self.base.middle, h_base, emb_b, ctx_rows, Bc, Lc, stats_last=False)
+        h_ctr = self.ctrl.run_layers(self.ctrl.middle, h_ctr, emb_c, ctx_rows, Bc, Lc, stats_last=False)
+        h_base = ops.conv2d(h_ctr, s.conv(self.mid_zero, scale=sc), res=h_base, stats=True)
+        nout = len(self.base.output_blocks)
         for i, lb in enumerate(self.base.output_blocks):
-            h_base = ops.conv2d(hs_ctr.pop(), s.conv(self.dec_zero[i], scale=sc), res=h_base)
-            h_base = self.base.run_layers(lb, h_base, emb_b, ctx_rows, Bc, Lc, x2=hs_base.pop())
+            h_base = ops.conv2d(hs_ctr.pop(), s.conv(self.dec_zero[i], scale=sc), res=h_base, stats=True)
+            h_base = self.base.run_layers(lb, h_base, emb_b, ctx_rows, Bc, Lc, x2=hs_base.pop(),
+                                          stats_last=(i + 1 == nout))
         p = self.base.prefix
         ab = ops.group_norm_ab(h_base, s.get(p + "out.0.weight"), s.get(p + "out.0.bias"), 32, 1e-5)
         return ops.conv2d(h_base, s.conv(p + "out.2"), gn=ab, gn_silu=True, out_f32=True)

@@ -95,10 +95,11 @@ class AutoencoderKL:
         pre, cin, cout = blk
         s = self.store
         ab1 = ops.group_norm_ab(x, s.get(pre + ".norm1.weight"), s.get(pre + ".norm1.bias"), 32, GN_EPS)
-        h = ops.conv2d(x, s.conv(pre + ".conv1"), gn=ab1, gn_silu=True)
+        h = ops.conv2d(x, s.conv(pre + ".conv1"), gn=ab1, gn_silu=True, stats=True)
         ab2 = ops.group_norm_ab(h, s.get(pre + ".norm2.weight"), s.get(pre + ".norm2.bias"), 32, GN_EPS)
         skip = x if cin == cout else ops.conv2d(x, s.conv(pre + ".nin_shortcut"))
-        return ops.conv2d(h, s.conv(pre + ".conv2"), gn=ab2, gn_silu=True, res=skip)
+        # every ResnetBlock output feeds a GroupNorm (next block, AttnBlock or norm_out)
+        return ops.conv2d(h, s.conv(pre + ".conv2"), gn=ab2, gn_silu=True, res=skip, stats=True)
 
     def attn(self, blk, x):
         pre, c = blk
@@ -111,21 +112,22 @@ class AutoencoderKL:
         o = torch.empty((B * L, C), dtype=x.dtype, device=x.device)
         ops.attention_single_head_materialized(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch=B, length=L,
                                                dim=C, scale=int(C) ** (-0.5))
-        out = ops.linear(o, s.conv(pre + ".proj_out"), res=x.contiguous().view(B * L, C))
-        return out.view(B, H, W_, C)
+        out = ops.linear(o, s.conv(pre + ".proj_out"), res=x.contiguous().view(B * L, C), stats_hw=L)
+        return ops.tokens_to_nhwc(out, B, H, W_)
 
     # ------------------------------------------------------------------ passes
     def encode_hc(self, x: torch.Tensor, out_mul: float = 1.0) -> torch.Tensor:
         """x: NHWC compute-dtype image in [-1, 1] ([B,H,W,3]); returns c * out_mul, [B,H/8,W/8,512]."""
         s = self.store
         e = self.prefix + "encoder."
-        h = ops.conv2d(x, s.conv(e + "conv_in", cin_pad=x.shape[3] if x.shape[3] > 3 else None))
+        h = ops.conv2d(x, s.conv(e + "conv_in", cin_pad=x.shape[3] if x.shape[3] > 3 else None), stats=True)
         for lvl, down in self.enc_blocks:
             for blk in lvl:
                 h = self.resnet(blk, h)
             if down is not None:
                 Hh, Ww = h.shape[1], h.shape[2]
-                h = ops.conv2d(h, s.conv(down, stride=2, pad=0), pad_t=0, pad_l=0, out_hw=(Hh // 2, Ww // 2))
+                h = ops.conv2d(h, s.conv(down, stride=2, pad=0), pad_t=0, pad_l=0, out_hw=(Hh // 2, Ww // 2),
+                               stats=True)
         h = self.resnet(self.enc_mid[0], h)
         h = self.attn(self.enc_mid[1], h)
         h = self.resnet(self.enc_mid[2], h)
@@ -137,7 +139,7 @@ class AutoencoderKL:
         s = self.store
         d = self.prefix + "decoder."
         z = ops.conv2d(z, s.conv(self.prefix + "post_quant_conv"))
-        h = ops.conv2d(z, s.conv(d + "conv_in"))
+        h = ops.conv2d(z, s.conv(d + "conv_in"), stats=True)
         h = self.resnet(self.dec_mid[0], h)
         h = self.attn(self.dec_mid[1], h)
         h = self.resnet(self.dec_mid[2], h)
@@ -145,6 +147,6 @@ class AutoencoderKL:
             for blk in lvl:
                 h = self.resnet(blk, h)
             if up is not None:
-                h = ops.conv2d(h, s.conv(up), up2=True)
+                h = ops.conv2d(h, s.conv(up), up2=True, stats=True)
         ab = ops.group_norm_ab(h, s.get(d + "norm_out.weight"), s.get(d + "norm_out.bias"), 32, GN_EPS)
         return ops.conv2d(h, s.conv(d + "conv_out"), gn=ab, gn_silu=True, out_f32=out_f32)
