@@ -824,8 +824,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, 
 }
 
 template <int BM, int BN, int WGM, int WGN, int S, int EP>
-__global__ __launch_bounds__(WGM * WGN * 64) void conv_dma_kernel(ConvArgs a, int tiles_n, unsigned bytes0,
-                                                                  unsigned bytes1, unsigned bytesw) {
+__device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1,
+                                              unsigned bytesw) {
   constexpr int NW = WGM * WGN, NT = NW * 64;
   constexpr int RB = 128;
   constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
@@ -1026,6 +1026,22 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_dma_kernel(ConvArgs a, in
   }
 }
 
+// Kernel entry points. Residency: 1024-thread blocks need <= 80 SGPRs for two blocks per CU (the
+// hardware admits floor(800 / (ceil(sgpr / 16) * 16 + 16)) waves per SIMD; MI355X_MICROARCH.md
+// "Residency"), so the 16-wave 128x128 tile (64 KB of LDS: two blocks fit) is built with its
+// SGPR budget capped; the others keep the compiler's allocation.
+template <int BM, int BN, int WGM, int WGN, int S, int EP>
+__global__ __launch_bounds__(WGM * WGN * 64) void conv_dma_kernel(ConvArgs a, int tiles_n, unsigned bytes0,
+                                                                  unsigned bytes1, unsigned bytesw) {
+  conv_dma_body<BM, BN, WGM, WGN, S, EP>(a, tiles_n, bytes0, bytes1, bytesw);
+}
+
+template <int BM, int BN, int WGM, int WGN, int S, int EP>
+__global__ __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_num_sgpr(80))) void conv_dma_kernel_2pc(
+    ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1, unsigned bytesw) {
+  conv_dma_body<BM, BN, WGM, WGN, S, EP>(a, tiles_n, bytes0, bytes1, bytesw);
+}
+
 // DMA-path eligibility: bf16, 16-byte-aligned 64-channel blocks, every buffer < 2 GiB.
 bool dma_ok(const rdeic_conv_desc* d, const ConvArgs& a, unsigned& b0, unsigned& b1, unsigned& bw) {
   if (d->dtype != 1 || d->gn_ab || (d->c0 % 64) || (d->c1 % 64) || (d->ld0 % 8) || ((uintptr_t)d->in0 % 16)) return false;
@@ -1067,7 +1083,11 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
   const long tiles = (long)cdiv(a.M, BM) * tn;
   dim3 grid((unsigned)tiles, 1, a.splits > 1 ? a.splits : a.batch);
   constexpr int lds = S * (BM + BN) * 128;
-  hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0, b1, bw);
+  if constexpr (WGM * WGN == 16 && S * (BM + BN) * 128 <= 80 * 1024)
+    hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0, b1,
+                       bw);
+  else
+    hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0, b1, bw);
   return launch_status();
 }
 
