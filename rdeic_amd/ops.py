@@ -553,24 +553,42 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
     return out
 
 
+# Score-buffer budget of the single-head (VAE, d=512) attention: the fp32 scores of one query
+# chunk never exceed it, so the buffer is O(chunk x L), not O(B x L^2) (at 1024x1024 one image's
+# full score matrix alone would be 16384^2 x 4 B = 1 GiB).
+SCORE_BUDGET_BYTES = 512 << 20
+
+
 def attention_single_head_materialized(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, *,
                                        batch: int, length: int, dim: int, scale: float) -> torch.Tensor:
-    """softmax(q k^T * scale) v for one head with a large head dim (VAE AttnBlock, d=512):
-    S = Q K^T (batched MFMA GEMM, fp32) -> row softmax -> O = P V (batched GEMM)."""
+    """softmax(q k^T * scale) v for one head with a large head dim (VAE AttnBlock, d=512,
+    model.py:181-205): per chunk of query rows (whole images while they fit the score budget,
+    else row blocks of one image), S = Q K^T (batched MFMA GEMM, fp32) -> row softmax -> O = P V
+    (batched GEMM). Every output row is computed exactly as without chunking (same k order)."""
     if dim % 64 != 0 or length % 64 != 0:
         raise ValueError("materialised attention needs dim, length multiples of 64")
     dt = dt_code(q)
-    s = torch.empty((batch, length, length), dtype=torch.float32, device=q.device)
-    gemm_batched(q, k, s, batch=batch, m=length, n=length, k=dim, lda=q.stride(0), ldb=k.stride(0),
-                 a_bs=length * q.stride(0), b_bs=length * k.stride(0), out_bs=length * length)
-    p = torch.empty((batch, length, length), dtype=q.dtype, device=q.device)
-    call("rdeic_softmax_rows", s.data_ptr(), batch * length, length, float(scale), p.data_ptr(), dt, stream_ptr())
-    del s
-    vt = torch.empty((batch, dim, length), dtype=q.dtype, device=q.device)
-    call("rdeic_transpose", v.data_ptr(), length, dim, v.stride(0), vt.data_ptr(), length, batch,
-         length * v.stride(0), dim * length, dt, stream_ptr())
-    gemm_batched(p, vt, out, batch=batch, m=length, n=dim, k=length, lda=length, ldb=length,
-                 a_bs=length * length, b_bs=dim * length, out_bs=length * out.stride(0))
+    L = length
+    per_img = L * L * 4
+    if per_img <= SCORE_BUDGET_BYTES:
+        g, qrows = max(1, min(batch, SCORE_BUDGET_BYTES // per_img)), L
+    else:
+        g, qrows = 1, max(64, (SCORE_BUDGET_BYTES // (L * 4)) // 64 * 64)
+    vt = torch.empty((batch, dim, L), dtype=q.dtype, device=q.device)
+    call("rdeic_transpose", v.data_ptr(), L, dim, v.stride(0), vt.data_ptr(), L, batch,
+         L * v.stride(0), dim * L, dt, stream_ptr())
+    s = torch.empty((g, qrows, L), dtype=torch.float32, device=q.device)
+    p = torch.empty((g, qrows, L), dtype=q.dtype, device=q.device)
+    for b0 in range(0, batch, g):
+        nb = min(g, batch - b0)
+        for q0 in range(0, L, qrows):
+            nq = min(qrows, L - q0)
+            qa = q[b0 * L + q0:]
+            gemm_batched(qa, k[b0 * L:], s, batch=nb, m=nq, n=L, k=dim, lda=q.stride(0), ldb=k.stride(0),
+                         a_bs=L * q.stride(0), b_bs=L * k.stride(0), out_bs=nq * L)
+            call("rdeic_softmax_rows", s.data_ptr(), nb * nq, L, float(scale), p.data_ptr(), dt, stream_ptr())
+            gemm_batched(p, vt[b0:], out[b0 * L + q0:], batch=nb, m=nq, n=dim, k=L, lda=L, ldb=L,
+                         a_bs=nq * L, b_bs=dim * L, out_bs=L * out.stride(0))
     return out
 
 
