@@ -35,5 +35,9 @@ clean:
 
 .PHONY: all clean oracle
 
+# attention: MFMA results in VGPRs (the softmax reads every score; in AGPRs each one costs a
+# v_accvgpr_read/write pair per tile, ~180 extra VALU instructions per 64-key tile)
+$(BUILD)/attention.hip.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form=1
+
 # parity-sensitive scalar kernels: no fma contraction anywhere in these TUs (headers included)
 $(BUILD)/elementwise.hip.o $(BUILD)/entropy.hip.o: HIPFLAGS += -ffp-contract=off

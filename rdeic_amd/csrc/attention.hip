@@ -637,6 +637,13 @@ __device__ __forceinline__ v4s ds_read_tr16(unsigned lds_addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
   return r;
 }
+// the same with an immediate byte offset (one base register serves several fragments)
+template <int OFF>
+__device__ __forceinline__ v4s ds_read_tr16_off(unsigned lds_addr) {
+  v4s r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lds_addr), "n"(OFF) : "memory");
+  return r;
+}
 
 template <int N>
 __device__ __forceinline__ void attn_wait_vm() {
@@ -707,7 +714,14 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) oacc[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY};
+  // Row sums on the matrix core: lsum[u] += ONES (16 x 32) . P^T (32 keys x 16 queries) gives every
+  // lane its query's sum of the bf16 probabilities (the ones that enter O), complete — no per-score
+  // fp32 add and no cross-lane reduction; the softmax VALU work per score drops by one add.
+  f32x4 lsum[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
 
   // fragment-read addressing (per lane constants)
   const int krk = ((((lr >> 3) & 1) << 1) | (((lr >> 1) & 1) << 2));  // K row key of rows 16t + lr
@@ -739,19 +753,20 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
     }
     // V^T fragments for O^T += V^T P^T, read now so the LDS latency hides under the softmax:
     // lane (lr, g) needs V[keys 32c + 4g + 0..3 (lo) / +16 (hi)][d = 16dt + lr]
+    // (row r = 32c + 16hl + 4g + vq: its swizzle ((r >> 1) & 3) << 1 depends on the lane only, so
+    // one base per dt and immediates (32c + 16hl) * 128 address all four reads of a dt)
     v4s vt[4][2][2];
     {
-      const unsigned vbase = (unsigned)(uintptr_t)(lds_vptr_t)Vt;
+      const unsigned vbase = (unsigned)(uintptr_t)(lds_vptr_t)Vt + (4 * g + vq) * 128 + (vp & 1) * 8;
+      const int swz = ((((4 * g + vq) >> 1) & 3) << 1);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int hl = 0; hl < 2; ++hl) {
-            const int r = 32 * c + 16 * hl + 4 * g + vq;
-            const int ch = 2 * dt + (vp >> 1);
-            vt[dt][c][hl] = ds_read_tr16(vbase + r * 128 + ((ch ^ (((r >> 1) & 3) << 1)) * 16) + (vp & 1) * 8);
-          }
+      for (int dt = 0; dt < 4; ++dt) {
+        const unsigned a = vbase + (((2 * dt + (vp >> 1)) ^ swz) * 16);
+        vt[dt][0][0] = ds_read_tr16_off<0>(a);
+        vt[dt][0][1] = ds_read_tr16_off<16 * 128>(a);
+        vt[dt][1][0] = ds_read_tr16_off<32 * 128>(a);
+        vt[dt][1][1] = ds_read_tr16_off<48 * 128>(a);
+      }
     }
     if (key0 + 64 > lk) {
 #pragma unroll
@@ -782,22 +797,19 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
         rescale = true;
       }
       const float nm = -m_run[u];
-      float ps = 0.f;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(st[u][2 * c + (j >> 2)][j & 3], scale_log2, nm));
-          ps += p;
-          pf[u][c][j] = (bf16)p;
-        }
-      l_run[u] = l_run[u] * alpha[u] + ps;
+        for (int j = 0; j < 8; ++j)
+          pf[u][c][j] = (bf16)__builtin_amdgcn_exp2f(fmaf(st[u][2 * c + (j >> 2)][j & 3], scale_log2, nm));
     }
     if (__any(rescale)) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) oacc[u][dt] *= alpha[u];
+        lsum[u] *= alpha[u];
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm transposed reads above
 #pragma unroll
@@ -810,13 +822,14 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
         for (int u = 0; u < 2; ++u) oacc[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[u][c], oacc[u][dt], 0, 0, 0);
       }
     }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) lsum[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[u][c], lsum[u], 0, 0, 0);
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    float l = l_run[u];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.f / l;
+    const float inv = 1.f / lsum[u][0];
     const int qq = qw + 16 * u + lr;
     if (qq < lq) {
       bf16* orow = o + ((long)b * lq + qq) * ldo + h * 64;

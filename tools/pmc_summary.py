@@ -16,7 +16,7 @@ def load(path):
 for path in sys.argv[1:]:
     print("==", path)
     for k, cs in load(path).items():
-        if "conv" not in k:
+        if "conv" not in k and "attn" not in k:
             continue
         short = k.split("(")[0][-90:]
         print("  ", short)
