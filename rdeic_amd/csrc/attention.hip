@@ -651,6 +651,7 @@ __device__ __forceinline__ void attn_wait_vm() {
 }
 
 constexpr int A64D_TILE = 64 * 128, A64D_STAGE = 2 * A64D_TILE, A64D_S = 3;
+template <int N> struct SlotC { static constexpr int value = N; };
 
 __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
                                                          int ldk, const bf16* __restrict__ v, int ldv,
@@ -697,8 +698,10 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
     kco[j] = (unsigned)(sl ^ ((((row >> 3) & 1) << 1) | (((row >> 1) & 1) << 2))) * 16u;
     vco[j] = (unsigned)(sl ^ (((row >> 1) & 3) << 1)) * 16u;
   }
-  auto issue = [&](int kt) {
-    char* sb = lds + (kt % A64D_S) * A64D_STAGE;
+  // the ring slot is a compile-time constant (the tile loop is unrolled by the ring depth), so every
+  // LDS address below is a per-lane base plus an immediate
+  auto issue = [&](int kt, auto slot) {
+    char* sb = lds + decltype(slot)::value * A64D_STAGE;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int key = kt * 64 + drow[j];
@@ -728,13 +731,14 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
   const int vq = lr >> 2, vp = lr & 3;                                    // tr-read: block row q, column group p
 
   const int ntiles = (lk + 63) / 64;
-  issue(0);
-  if (ntiles > 1) issue(1);
-  for (int kt = 0; kt < ntiles; ++kt) {
+  issue(0, SlotC<0>{});
+  if (ntiles > 1) issue(1, SlotC<1>{});
+  auto step = [&](int kt, auto slot) {
+    constexpr int SL = decltype(slot)::value;
     if (kt + 1 < ntiles) attn_wait_vm<4>(); else attn_wait_vm<0>();
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < ntiles) issue(kt + 2);
-    const char* Kt = lds + (kt % A64D_S) * A64D_STAGE;
+    if (kt + 2 < ntiles) issue(kt + 2, SlotC<(SL + 2) % A64D_S>{});
+    const char* Kt = lds + SL * A64D_STAGE;
     const char* Vt = Kt + A64D_TILE;
     const int key0 = kt * 64;
     f32x4 st[2][4];
@@ -826,6 +830,12 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int u = 0; u < 2; ++u) lsum[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[u][c], lsum[u], 0, 0, 0);
+  };
+  static_assert(A64D_S == 3, "the tile loop is unrolled by the ring depth");
+  for (int kt = 0; kt < ntiles; kt += 3) {
+    step(kt, SlotC<0>{});
+    if (kt + 1 < ntiles) step(kt + 1, SlotC<1>{});
+    if (kt + 2 < ntiles) step(kt + 2, SlotC<2>{});
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
