@@ -243,11 +243,17 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
     }
   }
   f32x4 oacc[NQ][NDT];
-  float m_run[NQ], l_part[NQ];
+  // row sums on the matrix core (ONES . P^T, as the d64 kernel): each lane gets its query's sum of
+  // the bf16 probabilities, complete, with no per-score add and no cross-lane reduction
+  f32x4 lsum[NQ];
+  float m_run[NQ];
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
     m_run[g] = -INFINITY;
-    l_part[g] = 0.f;
+    lsum[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < NDT; ++u) oacc[g][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -297,25 +303,25 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sacc[t][i]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m_run[g], mx);
-      const float alpha = __builtin_amdgcn_exp2f((m_run[g] - mnew) * scale_log2);
-      m_run[g] = mnew;
-      const float mneg = -mnew * scale_log2;
+      // deferred rescale: the running max moves only when a score exceeds it by more than 2^8 in
+      // exp2 units (probabilities <= 256 stay exact enough in fp32 / bf16), so most tiles skip the
+      // alpha exp and the accumulator rescale
+      if ((mx - m_run[g]) * scale_log2 > 8.f) {
+        const float alpha = __builtin_amdgcn_exp2f((m_run[g] - mx) * scale_log2);
+        m_run[g] = mx;
+        lsum[g] *= alpha;
+#pragma unroll
+        for (int u = 0; u < NDT; ++u) oacc[g][u] *= alpha;
+      }
+      const float mneg = -m_run[g] * scale_log2;
       bf16x8 pf[NS];
-      float ps = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[t][i], scale_log2, mneg));
-          ps += p;
-          pf[t >> 1][(t & 1) * 4 + i] = (bf16)p;
-        }
-      l_part[g] = l_part[g] * alpha + ps;
+        for (int i = 0; i < 4; ++i)
+          pf[t >> 1][(t & 1) * 4 + i] = (bf16)__builtin_amdgcn_exp2f(fmaf(sacc[t][i], scale_log2, mneg));
 #pragma unroll
-      for (int u = 0; u < NDT; ++u)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) oacc[g][u][i] *= alpha;
+      for (int s2 = 0; s2 < NS; ++s2) lsum[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[s2], lsum[g], 0, 0, 0);
       // O^T[d][q] += sum_k V^T[d][key(k)] P^T[key(k)][q]
 #pragma unroll
       for (int s = 0; s < NS; ++s)
@@ -331,10 +337,7 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
   }
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
-    float l = l_part[g];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.f / l;
+    const float inv = 1.f / lsum[g][0];
     const int myq = q0 + (wave * NQ + g) * 16 + lr;
     if (myq < lq) {
       bf16* orow = o + ((long)b * lq + myq) * ldo + h * DH;
