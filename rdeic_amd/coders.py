@@ -99,10 +99,19 @@ class GaussianTables:
 
 
 def default_threads() -> int:
+    """Host coder threads per call: the CPUs this process can use (affinity set, capped by the
+    cgroup CPU quota: a GPU box shows 256 CPUs but grants 16), at most 16."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
     return max(1, min(16, n))
 
 

@@ -309,8 +309,10 @@ int rans_decode_impl(RansDecoder* d, const int32_t* idx, size_t n, const int32_t
 // One job runs at a time (callers serialise on job_mu); the caller thread works too.
 class WorkerPool {
  public:
+  // one pool per calling thread: codec sessions on different host threads (bench.py --streams)
+  // code their images concurrently instead of queueing on one job lock
   static WorkerPool& get() {
-    static WorkerPool* p = new WorkerPool();  // intentionally leaked: workers outlive static dtors
+    thread_local WorkerPool* p = new WorkerPool();  // intentionally leaked: workers outlive thread dtors
     return *p;
   }
   void run(int32_t count, int32_t threads, const std::function<void(int32_t)>& f) {

@@ -316,11 +316,19 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
     return max(1, min(-(-512 // tiles), nk // 16, 8))
 
 
+_SPLITK_KEEP: list = []  # every workspace ever handed out: recorded launch plans hold their pointers
+
+
 def _splitk_workspace(n: int, device) -> torch.Tensor:
-    buf = _SPLITK_WS.get(device)
+    """Split-K partial-sum scratch, one per (device, stream): concurrent codec sessions (one per
+    stream) must not share it. A grown workspace replaces the old one for new launches, but the
+    old one stays allocated (plans recorded earlier still point at it)."""
+    key = (str(device), stream_ptr())
+    buf = _SPLITK_WS.get(key)
     if buf is None or buf.numel() < n:
         buf = torch.empty(n, dtype=torch.float32, device=device)
-        _SPLITK_WS[device] = buf
+        _SPLITK_WS[key] = buf
+        _SPLITK_KEEP.append(buf)
     return buf
 
 

@@ -127,11 +127,15 @@ class PlanCache:
             if before is not None:
                 before()
             out = plan.record(fn, *statics)
-            self.plans[key] = (plan, statics)
+            self.plans[key] = (plan, statics, ops.stream_ptr())
             return out
+        plan, statics, stream = ent
+        if stream != ops.stream_ptr():
+            # the recorded launches (and the events of its host steps) are bound to that stream
+            raise RuntimeError("launch plan replayed on a different stream than it was recorded on: "
+                               "use one RDEIC.session() per stream")
         if before is not None:
             before()
-        plan, statics = ent
         for s, t in zip(statics, inputs):
             if s.data_ptr() != t.data_ptr():
                 s.copy_(t)

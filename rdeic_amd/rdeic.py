@@ -100,6 +100,23 @@ class RDEIC:
         self._use_plans = bool(v)
         self.preprocess_model.use_plans = bool(v)
 
+    def session(self) -> "RDEIC":
+        """A codec session sharing this model's weights, tables and kernels but with its own launch
+        plans, pinned buffers and per-call host state: one session per host thread / HIP stream lets
+        two batches be in flight at once (one batch's host entropy coding overlaps the other's GPU
+        work). Record each session's plans (run it once) before running sessions concurrently."""
+        import copy
+        from .plan import PlanCache
+        s = copy.copy(self)
+        s._plans = PlanCache()
+        s._consts = {}
+        pm = copy.copy(self.preprocess_model)
+        pm._plans = PlanCache()
+        pm._io = {}
+        pm.__dict__.pop("_pin_cache", None)
+        s.preprocess_model = pm
+        return s
+
     def _clear_plans(self):
         self._plans.clear()
         self.preprocess_model._plans.clear()
