@@ -82,7 +82,7 @@ def parse():
 
 def main():
     args = parse()
-    from rdeic_amd import ops, parallel
+    from rdeic_amd import metrics as quality, ops, parallel
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import relay_noise, synth_context, synth_image
 
@@ -126,9 +126,10 @@ def main():
                                         step_noise_nchw=step_noise)
         ops.call("rdeic_image_mse", imgs.data_ptr(), out.data_ptr(), B, S * S * 3, mse.data_ptr(), ops.stream_ptr())
         m = mse.cpu().numpy()
+        _, ms = quality.ssim_ms_ssim(out, imgs)  # on the device (rdeic_image_ssim)
         return torch.tensor([[len(b) * 8.0 / (S * S), float(len(b)),
-                              10 * math.log10(255.0 ** 2 / max(float(v), 1e-10)), float(v), 1.0, float(rank)]
-                             for b, v in zip(bodies, m)], dtype=torch.float32)
+                              10 * math.log10(255.0 ** 2 / max(float(v), 1e-10)), float(v), float(q), 1.0, float(rank)]
+                             for b, v, q in zip(bodies, m, ms)], dtype=torch.float32)
 
     def log(msg):  # progress on stderr (the JSON line is the only stdout)
         if rank == 0:
@@ -201,6 +202,7 @@ def main():
         mrows = metrics.cpu().numpy()
         results.append({"target_bpp": target, "rate_gain": rate_gain, "elapsed": elapsed, "prof": prof,
                         "mean_bpp": float(mrows[:, 0].mean()), "mean_psnr_db": float(mrows[:, 2].mean()),
+                        "mean_ms_ssim": float(mrows[:, 4].mean()),
                         "images": int(mrows.shape[0])})
         del sessions
     parallel.finish()  # every rank leaves the group before rank 0's CPU-baseline leg
@@ -261,7 +263,8 @@ def main():
                                f"{'DDIM' if args.sampler == 'ddim' else 'spaced DDPM'}, "
                                f"encode+entropy-code+decode+VAE-decode", "global_batch": G,
                    "image_size": S, "ddim_steps": args.ddim_steps, "sampler": args.sampler, "parallelism": f"dp{world}", "codec_sessions_per_gpu": nsess, "rate_gain": rate_gain,
-                   "mean_bpp": round(r["mean_bpp"], 4), "mean_psnr_db": round(r["mean_psnr_db"], 2)},
+                   "mean_bpp": round(r["mean_bpp"], 4), "mean_psnr_db": round(r["mean_psnr_db"], 2),
+                   "mean_ms_ssim": round(r["mean_ms_ssim"], 4)},
         "roofline": roof,
         "cpu_baseline": cpu,
     }

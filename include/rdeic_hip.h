@@ -228,6 +228,17 @@ int rdeic_gather_rows(const float* table, int32_t ld_table, const int32_t* idx, 
 int rdeic_row_sqnorm(const void* x, int32_t rows, int32_t dim, int32_t ld, float* out, int32_t dtype,
                      void* stream);
 
+/* ------------------------------------------------------------ image quality
+ * SSIM / MS-SSIM of uint8 RGB image pairs [n][h][w][3] (the reference's pyiqa "ssim" / "ms_ssim"
+ * with test_y_channel, experiments/run_robustness.py:70-83; restated, parity unpinned): YIQ luma
+ * rounded to integers, 11x11 Gaussian (sigma 1.5) 'valid' windows, data range 255, `levels` scales
+ * with 2x2 average pooling between them. out[img][level][2] = (mean ssim, mean relu'd cs) of each
+ * level; SSIM = out[.][0][0], MS-SSIM = prod_{l<4} cs_l^w_l * ssim_4^w_4 (host).
+ * ws: rdeic_image_ssim_ws_floats(n, h, w, levels) floats of device scratch. */
+size_t rdeic_image_ssim_ws_floats(int32_t n, int32_t h, int32_t w, int32_t levels);
+int rdeic_image_ssim(const uint8_t* a, const uint8_t* b, int32_t n, int32_t h, int32_t w, int32_t levels, float* ws,
+                     size_t ws_floats, float* out, void* stream);
+
 /* ------------------------------------------------------------ host coders
  * Gaussian-conditional tables (compressai 1.2.4 GaussianConditional.update, precision 16).
  * pmf: [levels][pmf_ld] float32 pmf rows of length pmf_len[i] followed by the tail mass

@@ -101,6 +101,8 @@ PROTOTYPES = {
     "rdeic_build_gaussian_tables": (C.c_int, [_p, _p, _i32, _i32, _p, _i32, _p, _p]),
     "rdeic_rans_encode": (C.c_int, [_p, _p, _sz, _p, _i32, _p, _p, _i32, _p, _sz, C.POINTER(_sz)]),
     "rdeic_rans_encode_batch": (C.c_int, [_i32, _p, _p, _sz, _sz, _p, _i32, _p, _p, _i32, _p, _sz, _p, _i32]),
+    "rdeic_image_ssim_ws_floats": (C.c_size_t, [_i32, _i32, _i32, _i32]),
+    "rdeic_image_ssim": (C.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, C.c_size_t, _p, _p]),
     "rdeic_groupnorm_parts_floats": (C.c_size_t, [_i64, _i32, _i32]),
     "rdeic_groupnorm_parts_ab": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p]),
     "rdeic_rans_enc_tables_create": (_p, [_p, _i32, _p, _p, _i32]),

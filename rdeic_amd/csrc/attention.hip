@@ -635,12 +635,7 @@ __device__ __forceinline__ void attn_dma16(__amdgpu_buffer_rsrc_t rs, char* lds_
 // ds_read_b64_tr_b16 as inline asm: through the builtin, hipcc treats the read as aliasing the
 // in-flight LDS-DMA and drains vmcnt(0) before it (ending the prefetch). The caller waits
 // lgkmcnt itself before using the result (hipcc does not count asm LDS operations).
-__device__ __forceinline__ v4s ds_read_tr16(unsigned lds_addr) {
-  v4s r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
-  return r;
-}
-// the same with an immediate byte offset (one base register serves several fragments)
+// (with an immediate byte offset: one base register serves several fragments)
 template <int OFF>
 __device__ __forceinline__ v4s ds_read_tr16_off(unsigned lds_addr) {
   v4s r;

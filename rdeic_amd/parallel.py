@@ -11,7 +11,7 @@ from typing import Tuple
 import torch
 import torch.distributed as dist
 
-METRIC_FIELDS = ("bpp", "bytes", "psnr", "mse", "decode_ok", "rank")
+METRIC_FIELDS = ("bpp", "bytes", "psnr", "mse", "ms_ssim", "decode_ok", "rank")
 
 
 def init_from_env(backend: str = None) -> Tuple[int, int, int]:

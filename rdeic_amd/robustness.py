@@ -151,8 +151,9 @@ def run_bitstream_robustness(model, img_u8: torch.Tensor, context: torch.Tensor,
                              mean_burst_len: float = 8.0) -> List[Dict]:
     """Encode each image once, corrupt its bitstream per (rate, seed), decode every corrupted body,
     relay-decode all survivors in one batch, and score PSNR against the original pixels. Returns
-    one record per (image, rate, seed) with the reference's columns (ssim / ms_ssim / lpips are
-    None: those metrics need pyiqa / AlexNet weights, out of scope)."""
+    one record per (image, rate, seed) with the reference's columns: PSNR, and SSIM / MS-SSIM on
+    the device (rdeic_amd/metrics.py; images of at least 176 pixels a side) — lpips stays None (it
+    needs AlexNet weights, not available offline)."""
     B, H, W, _ = img_u8.shape
     ids = list(image_ids) if image_ids is not None else [f"img{i}" for i in range(B)]
     bodies = model.compress_images(img_u8)
@@ -186,9 +187,17 @@ def run_bitstream_robustness(model, img_u8: torch.Tensor, context: torch.Tensor,
             step_noise = torch.stack([ops.nchw_to_nhwc(torch.randn((n, 4, c_lat.shape[1], c_lat.shape[2]),
                                                                    generator=gen).to(c_lat.device), torch.float32)
                                       for _ in range(steps)])
-        out = model.relay_decode_u8(c_lat, gh, context, noise, steps, sampler, step_noise).cpu().numpy()
+        out_d = model.relay_decode_u8(c_lat, gh, context, noise, steps, sampler, step_noise)
+        out = out_d.cpu().numpy()
+        tgt = img_u8.to(out_d.device)[torch.tensor([i for i, _ in ok], device=out_d.device)]
+        ssim, ms_ssim = (None, None)
+        if min(H, W) >= 176:  # 5 MS-SSIM scales need >= 11 pixels at the coarsest one
+            from .metrics import ssim_ms_ssim
+            ssim, ms_ssim = ssim_ms_ssim(out_d, tgt)
         for k, (i, rec) in enumerate(ok):
             rec["psnr"] = psnr_u8(out[k], ref[i])
+            if ssim is not None:
+                rec["ssim"], rec["ms_ssim"] = float(ssim[k]), float(ms_ssim[k])
     return [rec for _, rec in jobs]
 
 
