@@ -1,0 +1,56 @@
+"""inference_partition.py (reference inference_partition.py:139-571): images grouped by padded
+size, batched, micro-batched relay decode, per-image bitstream files, metrics.csv; results must not
+depend on the batching (per-image noise seeds, fp32 parity path), and the resize guard must
+upsample outputs back to the original size."""
+import csv
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_inputs(d):
+    from PIL import Image
+    from rdeic_amd.synthetic import synth_image
+    os.makedirs(d, exist_ok=True)
+    Image.fromarray(synth_image(128, 128, 11)).save(os.path.join(d, "a.png"))
+    Image.fromarray(synth_image(128, 128, 12)).save(os.path.join(d, "b.png"))
+    Image.fromarray(synth_image(96, 160, 13)[:, :, :]).save(os.path.join(d, "c.png"))  # 96 high, 160 wide
+
+
+def test_partition_batching_is_invariant_and_writes_metrics(gpu, tmp_path):
+    import inference_partition as P
+    from PIL import Image
+    src = str(tmp_path / "in")
+    _write_inputs(src)
+    base = ["--input", src, "--sampler", "ddim", "--steps", "2"]
+    r2 = P.main(base + ["--output", str(tmp_path / "o2"), "--batch_size", "2", "--micro_batch_size", "1"])
+    r1 = P.main(base + ["--output", str(tmp_path / "o1"), "--batch_size", "1"])
+    assert [r["image"] for r in r2] == ["a.png", "b.png", "c.png"]  # groups (128,128) then (128,192)
+    for name in ("a", "b", "c"):
+        x2 = np.array(Image.open(tmp_path / "o2" / f"{name}.png"))
+        x1 = np.array(Image.open(tmp_path / "o1" / f"{name}.png"))
+        assert np.array_equal(x1, x2), name
+        body = (tmp_path / "o2" / "data" / name).read_bytes()
+        assert (tmp_path / "o1" / "data" / name).read_bytes() == body
+    sizes = {"a": (128, 128), "b": (128, 128), "c": (96, 160)}
+    with open(tmp_path / "o2" / "metrics.csv") as f:
+        rows = list(csv.DictReader(f))
+    assert [r["image"] for r in rows] == ["a.png", "b.png", "c.png"]
+    for r in rows:
+        name = r["image"][0]
+        h, w = sizes[name]
+        ph, pw = -(-h // 64) * 64, -(-w // 64) * 64
+        nbytes = (tmp_path / "o2" / "data" / name).stat().st_size
+        assert abs(float(r["bpp"]) - 8.0 * nbytes / (ph * pw)) < 1e-9
+        assert np.isfinite(float(r["psnr"])) and r["lpips"] == "nan"
+        assert np.array(Image.open(tmp_path / "o2" / f"{name}.png")).shape == (h, w, 3)
+    # resize guard: 160-wide image downscaled to 96 on its long side, output upsampled back
+    rg = P.main(base + ["--output", str(tmp_path / "og"), "--enable_resize_guard", "--max_long_side", "96",
+                        "--upsample_to_original", "--save_intermediates"])
+    c = [r for r in rg if r["image"] == "c.png"][0]
+    assert c["scale"] < 1.0
+    assert np.array(Image.open(tmp_path / "og" / "c.png")).shape == (96, 160, 3)
+    assert (tmp_path / "og" / "c_latent.pt").exists() and (tmp_path / "og" / "c_guide.png").exists()
