@@ -306,6 +306,112 @@ int rdeic_prof_start(int32_t capacity, int32_t every);
 int rdeic_prof_stop(void);
 int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms);
 
+/* ------------------------------------------------ adapter fine-tune step (config 5, train.hip)
+ * Replace the autograd backward of the modules the reference's fine-tune trains or back-propagates
+ * through (model/rdeic.py:763-881 configure_optimizers / p_losses, model/compression.py:52-149,
+ * model/compression_modules.py:228-307, ldm/modules/diffusionmodules/openaimodel.py:162-274,
+ * ldm/modules/attention.py:49-56,153-203,255-285) and torch.optim.AdamW.
+ *
+ * Strided batched GEMM on MFMA: C[z](i,j) = alpha * sum_kk A[z](i,kk) B[z](kk,j) + beta * C[z](i,j),
+ * A(i,kk) = a[i*a_sm + kk*a_sk], B(kk,j) = b[kk*b_sk + j*b_sn], C(i,j) = c[i*c_sm + j]; batch
+ * z = z1*nb2 + z2 adds z1*x_bs1 + z2*x_bs2 to every operand. ksplit > 0: z1 selects the k-range
+ * [z1*ksplit, (z1+1)*ksplit) instead (A/B bs1 unused; C plane z1*c_bs1), for split-K weight
+ * gradients. dtype 0 fp32 / 1 bf16 inputs; c_f32 = 1 writes fp32 C. */
+typedef struct rdeic_gemm_desc {
+  const void* a;
+  int64_t a_bs1, a_bs2, a_sm, a_sk;
+  const void* b;
+  int64_t b_bs1, b_bs2, b_sk, b_sn;
+  void* c;
+  int64_t c_bs1, c_bs2, c_sm;
+  int32_t batch, nb2, m, n, k, ksplit, dtype, c_f32;
+  float alpha, beta;
+} rdeic_gemm_desc;
+int rdeic_gemm_strided(const rdeic_gemm_desc* d, void* stream);
+/* conv input gradient = the forward conv of dy with this flipped / transposed packing of the fp32
+ * torch-layout weight [cout][cin][kh][kw] ([cin][wld], K order (ky, kx, co)) and pad kh-1-pad;
+ * stride 2: dy zero-inserted first; nearest-up input: the 2x2 sums of the gradient (sum_pool2);
+ * PixelShuffle(2) output: pixel_unshuffle2 of the gradient first. h, w are the small grid. */
+int rdeic_pack_conv_weight_dgrad(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw, void* out,
+                                 int32_t wld, int32_t to_bf16, void* stream);
+int rdeic_zero_insert2(const void* src, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, void* dst,
+                       int32_t dst_ld, int32_t dtype, void* stream);
+int rdeic_sum_pool2(const void* src, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, void* dst,
+                    int32_t dst_ld, int32_t dtype, void* stream);
+int rdeic_pixel_unshuffle2(const void* src, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, void* dst,
+                           int32_t dst_ld, int32_t dtype, void* stream);
+/* weight gradient: im2col rows [p][(ky,kx,ci)] of the conv input, the split-K GEMM dy^T . cols, then
+ * the sum of the split planes written (or added) in torch layout [cout][cin][kh][kw] */
+int rdeic_im2col(const void* x, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, int32_t kh, int32_t kw,
+                 int32_t stride, int32_t pad_t, int32_t pad_l, int32_t ho, int32_t wo, int32_t up2, void* out,
+                 int64_t out_ld, int32_t dtype, void* stream);
+int rdeic_wgrad_finalize(const float* part, int32_t splits, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
+                         float* dw, int32_t accumulate, void* stream);
+/* out[g][c] (+)= sum of the rows of group g (rows split into `groups` equal runs): bias / emb grads */
+size_t rdeic_col_sum_ws_floats(int64_t rows, int32_t c, int32_t groups);
+int rdeic_col_sum(const void* x, int64_t rows, int32_t c, int32_t ld, int32_t groups, float* out, int32_t accumulate,
+                  float* ws, size_t ws_floats, int32_t dtype, void* stream);
+/* act: 1 leaky (slope), 2 exact GELU, 3 SiLU. fwd: out = act(z) (+ res); bwd: dz = dy * act'(z) */
+int rdeic_act_fwd(const void* z, int64_t rows, int32_t c, int32_t ldz, const void* res, int32_t ldr, int32_t act,
+                  float slope, void* out, int32_t ldo, int32_t dtype, void* stream);
+int rdeic_act_bwd(const void* dy, int32_t ldy, const void* z, int32_t ldz, int64_t rows, int32_t c, int32_t act,
+                  float slope, void* dz, int32_t lddz, int32_t dtype, void* stream);
+/* GroupNorm training forward: mean / rstd per (image, group) -> mr [n][g][2] and the affine
+ * ab [n][c][2] (apply with rdeic_groupnorm_apply); backward (+ SiLU when silu) -> dx, dgamma,
+ * dbeta (null: not wanted). ws: rdeic_gn_train_ws_doubles; coef: [n][g][2] floats. */
+size_t rdeic_gn_train_ws_doubles(int32_t n, int32_t hw, int32_t c);
+int rdeic_gn_train_fwd(const void* x, int32_t ldx, int32_t n, int32_t hw, int32_t c, int32_t groups, float eps,
+                       const float* gamma, const float* beta, float* mr, float* ab, double* ws, int32_t dtype,
+                       void* stream);
+int rdeic_gn_train_bwd(const void* x, int32_t ldx, const void* dy, int32_t ldy, int32_t n, int32_t hw, int32_t c,
+                       int32_t groups, const float* mr, const float* gamma, const float* beta, int32_t silu, void* dx,
+                       int32_t lddx, float* dgamma, float* dbeta, int32_t accumulate, double* ws, float* coef,
+                       int32_t dtype, void* stream);
+/* LayerNorm backward (statistics recomputed); dgamma / dbeta optional (ws then required) */
+size_t rdeic_layernorm_bwd_ws_floats(int64_t rows, int32_t c);
+int rdeic_layernorm_bwd(const void* x, int32_t ldx, int64_t rows, int32_t c, const float* gamma, float eps,
+                        const void* dy, int32_t ldy, void* dx, int32_t lddx, float* dgamma, float* dbeta,
+                        int32_t accumulate, float* ws, size_t ws_floats, int32_t dtype, void* stream);
+/* ds = p * (dp - rowsum(p * dp)) * scale  (p [rows][cols] of rdeic_softmax_rows, dp fp32) */
+int rdeic_softmax_bwd_rows(const void* p, const float* dp, int64_t rows, int32_t cols, float scale, void* ds,
+                           int32_t dtype, void* stream);
+/* GEGLU backward: x = [value | gate] [rows][2c], dy [rows][c] -> dx [rows][2c] */
+int rdeic_geglu_bwd(const void* x, int32_t ldx, int64_t rows, int32_t c, const void* dy, int32_t ldy, void* dx,
+                    int32_t lddx, int32_t dtype, void* stream);
+/* checkerboard entropy slice in training mode (compression.py:80-139; compressai 1.2.4
+ * GaussianConditional noise-mode likelihood, LowerBound(0.11) scale, LowerBound(1e-9) likelihood,
+ * quantize_ste). Params [scales (c) | means (c)] per pixel; anchors at (row + col) odd.
+ *   anchor:   out = anchor ? round(y - mu_a) + mu_a : 0
+ *   lik:      out2 = (sum ln lik(y + noise), sum ln lik(round(y - mu) + mu)); nonanchor_hat likewise
+ *   lik_bwd:  from dL/d(sum ln lik) (device scalar) and d nonanchor_hat -> dy, dpa, dpn */
+int rdeic_ckbd_train_anchor(const void* y, int32_t ldy, const void* pa, int32_t ldpa, int32_t n, int32_t h, int32_t w,
+                            int32_t c, void* out, int32_t ldo, int32_t dtype, void* stream);
+/* out = x at anchor (which = 1) / non-anchor (which = 0) positions, 0 elsewhere */
+int rdeic_ckbd_mask(const void* x, int32_t ldx, int32_t n, int32_t h, int32_t w, int32_t c, int32_t which, void* out,
+                    int32_t ldo, int32_t dtype, void* stream);
+size_t rdeic_ckbd_train_ws_doubles(int32_t n, int32_t h, int32_t w, int32_t c);
+int rdeic_ckbd_train_lik(const void* y, int32_t ldy, const void* pa, int32_t ldpa, const void* pn, int32_t ldpn,
+                         const float* noise, int32_t n, int32_t h, int32_t w, int32_t c, void* nonanchor_hat,
+                         int32_t ldo, double* ws, float* out2, int32_t dtype, void* stream);
+int rdeic_ckbd_train_lik_bwd(const void* y, int32_t ldy, const void* pa, int32_t ldpa, const void* pn, int32_t ldpn,
+                             const float* noise, int32_t n, int32_t h, int32_t w, int32_t c, const float* g_sum,
+                             const void* d_nonanchor, int32_t ldd, void* dy, int32_t lddy, void* dpa, int32_t lddpa,
+                             void* dpn, int32_t lddpn, int32_t dtype, void* stream);
+/* VectorQuantiser.forward (training, anchor 'closest', contrastive loss) per code e, from
+ * dot = z . E^T [P][K], |z_p|^2, |E_e|^2 and the nearest-code indexes: re-initialises E and
+ * embed_prob in place, writes code_out [K][2] (CE_e, commitment sq-dist), dE_unit [K][D]
+ * (d emb_loss / dE for upstream gradient 1) and loss3 = (emb_loss, mse, mean CE). P <= 4096,
+ * D <= 512. vq_z_grad: dz = dzq + g_loss * coef * (z - zq). scale_dev: y (+)= s[0] * x. */
+int rdeic_vq_train(const float* dot, const float* zn, const float* en, const float* z, const int32_t* idx, int32_t P,
+                   int32_t K, int32_t D, float* E, float* embed_prob, float beta, float decay, float temp,
+                   float* code_out, float* dE_unit, float* loss3, void* stream);
+int rdeic_vq_z_grad(const float* z, const float* zq, const void* dzq, int64_t count, const float* g_loss, float coef,
+                    void* dz, int32_t dtype, void* stream);
+int rdeic_scale_dev(const float* x, int64_t count, const float* s, float* y, int32_t accumulate, void* stream);
+/* torch.optim.AdamW (decoupled weight decay) over flat fp32 buffers, step >= 1 */
+int rdeic_adamw(float* p, const float* g, float* m, float* v, int64_t count, float lr, float beta1, float beta2,
+                float eps, float weight_decay, int32_t step, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,18 @@ class ConvDesc(C.Structure):
     ]
 
 
+class GemmDesc(C.Structure):
+    """Mirror of rdeic_gemm_desc (strided batched GEMM, train.hip)."""
+    _fields_ = [
+        ("a", C.c_void_p), ("a_bs1", C.c_int64), ("a_bs2", C.c_int64), ("a_sm", C.c_int64), ("a_sk", C.c_int64),
+        ("b", C.c_void_p), ("b_bs1", C.c_int64), ("b_bs2", C.c_int64), ("b_sk", C.c_int64), ("b_sn", C.c_int64),
+        ("c", C.c_void_p), ("c_bs1", C.c_int64), ("c_bs2", C.c_int64), ("c_sm", C.c_int64),
+        ("batch", C.c_int32), ("nb2", C.c_int32), ("m", C.c_int32), ("n", C.c_int32), ("k", C.c_int32),
+        ("ksplit", C.c_int32), ("dtype", C.c_int32), ("c_f32", C.c_int32),
+        ("alpha", C.c_float), ("beta", C.c_float),
+    ]
+
+
 _p, _i32, _i64, _u64, _f, _sz = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_size_t
 
 # name -> (restype, argtypes). Every symbol of include/rdeic_hip.h appears here.
@@ -116,6 +128,39 @@ PROTOTYPES = {
     "rdeic_ac_encode": (C.c_int, [_p, _sz, _p, _i32, _p, _sz, C.POINTER(_sz)]),
     "rdeic_ac_decode": (C.c_int, [_p, _sz, _sz, _p, _i32, _p]),
     "rdeic_ac_uniform_cdf": (C.c_int, [_i32, _p]),
+    # adapter fine-tune step (train.hip)
+    "rdeic_gemm_strided": (C.c_int, [C.POINTER(GemmDesc), _p]),
+    "rdeic_pack_conv_weight_dgrad": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
+    "rdeic_zero_insert2": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
+    "rdeic_sum_pool2": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
+    "rdeic_pixel_unshuffle2": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
+    "rdeic_im2col": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p,
+                               _i64, _i32, _p]),
+    "rdeic_wgrad_finalize": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p]),
+    "rdeic_col_sum_ws_floats": (_sz, [_i64, _i32, _i32]),
+    "rdeic_col_sum": (C.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i32, _p, _sz, _i32, _p]),
+    "rdeic_act_fwd": (C.c_int, [_p, _i64, _i32, _i32, _p, _i32, _i32, _f, _p, _i32, _i32, _p]),
+    "rdeic_act_bwd": (C.c_int, [_p, _i32, _p, _i32, _i64, _i32, _i32, _f, _p, _i32, _i32, _p]),
+    "rdeic_gn_train_ws_doubles": (_sz, [_i32, _i32, _i32]),
+    "rdeic_gn_train_fwd": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p, _p, _i32, _p]),
+    "rdeic_gn_train_bwd": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p, _i32, _p, _p,
+                                     _i32, _p, _p, _i32, _p]),
+    "rdeic_layernorm_bwd_ws_floats": (_sz, [_i64, _i32]),
+    "rdeic_layernorm_bwd": (C.c_int, [_p, _i32, _i64, _i32, _p, _f, _p, _i32, _p, _i32, _p, _p, _i32, _p, _sz, _i32,
+                                      _p]),
+    "rdeic_softmax_bwd_rows": (C.c_int, [_p, _p, _i64, _i32, _f, _p, _i32, _p]),
+    "rdeic_geglu_bwd": (C.c_int, [_p, _i32, _i64, _i32, _p, _i32, _p, _i32, _i32, _p]),
+    "rdeic_ckbd_train_anchor": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
+    "rdeic_ckbd_mask": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
+    "rdeic_ckbd_train_ws_doubles": (_sz, [_i32, _i32, _i32, _i32]),
+    "rdeic_ckbd_train_lik": (C.c_int, [_p, _i32, _p, _i32, _p, _i32, _p, _i32, _i32, _i32, _i32, _p, _i32, _p, _p,
+                                       _i32, _p]),
+    "rdeic_ckbd_train_lik_bwd": (C.c_int, [_p, _i32, _p, _i32, _p, _i32, _p, _i32, _i32, _i32, _i32, _p, _p, _i32, _p,
+                                           _i32, _p, _i32, _p, _i32, _i32, _p]),
+    "rdeic_vq_train": (C.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _f, _f, _f, _p, _p, _p, _p]),
+    "rdeic_vq_z_grad": (C.c_int, [_p, _p, _p, _i64, _p, _f, _p, _i32, _p]),
+    "rdeic_scale_dev": (C.c_int, [_p, _i64, _p, _p, _i32, _p]),
+    "rdeic_adamw": (C.c_int, [_p, _p, _p, _p, _i64, _f, _f, _f, _f, _f, _i32, _p]),
 }
 
 _lib = None

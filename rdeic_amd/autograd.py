@@ -1,0 +1,647 @@
+"""Differentiable ops of the adapter fine-tune step (config 5), each a torch.autograd.Function whose
+forward AND backward run on the HIP kernels of librdeic_hip.so (train.hip, conv_gemm.hip, norm.hip,
+attention.hip). torch's autograd engine only sequences them and accumulates gradients.
+
+Layout: activations NHWC (channel-contiguous, pixel stride ld), token tensors [rows, c] with a row
+stride; weights are the fp32 masters in torch layout ([cout, cin, kh, kw] / [cout, cin]) so weight
+gradients land where torch.optim / the reference's checkpoints expect them. Activations (and their
+gradients) are in the compute dtype (fp32 parity mode or bf16); weight / bias / norm-parameter
+gradients are fp32.
+
+Backward formulations (reference modules whose autograd they replace are cited per op):
+  conv   dX = conv(dY, W flipped/transposed, pad k-1-p) on the forward implicit-GEMM kernel (stride 2:
+         dY zero-inserted; nearest-up input: 2x2 sum of the result); dW = split-K GEMM dY^T . im2col(X);
+         db / d(timestep emb) = column sums of dY
+  norms  GroupNorm(+SiLU) / LayerNorm closed-form backward with the saved / recomputed statistics
+  attn   materialised softmax(QK^T s) V: dP = dO V^T, dS = P (dP - rowsum(P dP)) s, dQ = dS K,
+         dK = dS^T Q, dV = P^T dO, all strided batched MFMA GEMMs over (image, head)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib, ops
+from ._lib import GemmDesc, call
+
+NONE, LEAKY, GELU, SILU = ops.NONE, ops.LEAKY, ops.GELU, ops.SILU
+
+
+def _dt(t: torch.Tensor) -> int:
+    return ops.dt_code(t)
+
+
+def _sp() -> int:
+    return ops.stream_ptr()
+
+
+def gemm(a, a_off: int, a_sm: int, a_sk: int, b, b_off: int, b_sk: int, b_sn: int, c, c_off: int, c_sm: int, *,
+         m: int, n: int, k: int, batch: int = 1, nb2: int = 1, a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0),
+         ksplit: int = 0, alpha: float = 1.0, beta: float = 0.0) -> None:
+    """rdeic_gemm_strided on tensors: element offsets / strides in elements of each tensor."""
+    if a.dtype != b.dtype:
+        raise TypeError("gemm operands must share a dtype")
+    if c.dtype not in (torch.float32, a.dtype):
+        raise TypeError("gemm output must be fp32 or the input dtype")
+    d = GemmDesc()
+    ea, eb, ec = a.element_size(), b.element_size(), c.element_size()
+    d.a, d.a_bs1, d.a_bs2, d.a_sm, d.a_sk = a.data_ptr() + a_off * ea, a_bs[0], a_bs[1], a_sm, a_sk
+    d.b, d.b_bs1, d.b_bs2, d.b_sk, d.b_sn = b.data_ptr() + b_off * eb, b_bs[0], b_bs[1], b_sk, b_sn
+    d.c, d.c_bs1, d.c_bs2, d.c_sm = c.data_ptr() + c_off * ec, c_bs[0], c_bs[1], c_sm
+    d.batch, d.nb2, d.m, d.n, d.k, d.ksplit = batch, nb2, m, n, k, ksplit
+    d.dtype = _dt(a)
+    d.c_f32 = int(c.dtype == torch.float32 and a.dtype != torch.float32)
+    d.alpha, d.beta = alpha, beta
+    call("rdeic_gemm_strided", C.byref(d), _sp())
+
+
+def col_sum(x2d_ptr_tensor: torch.Tensor, rows: int, c: int, ld: int, groups: int = 1, out=None,
+            accumulate: bool = False) -> torch.Tensor:
+    """[groups, c] fp32 sums over equal row groups of a [rows][ld] view (bias / emb gradients)."""
+    if out is None:
+        out = torch.empty((groups, c), dtype=torch.float32, device=x2d_ptr_tensor.device)
+    nws = int(_lib.load().rdeic_col_sum_ws_floats(rows, c, groups))
+    ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x2d_ptr_tensor.device)
+    call("rdeic_col_sum", x2d_ptr_tensor.data_ptr(), rows, c, ld, groups, out.data_ptr(), int(accumulate),
+         ws.data_ptr(), nws, _dt(x2d_ptr_tensor), _sp())
+    return out
+
+
+def _rows_view(t: torch.Tensor):
+    """(rows, c, ld) of an NHWC activation or a [rows, c] token tensor (channel-contiguous)."""
+    if t.dim() == 4:
+        ld = ops.pix_ld(t)
+        return t.shape[0] * t.shape[1] * t.shape[2], t.shape[3], ld
+    if t.dim() == 2 and t.stride(1) == 1:
+        return t.shape[0], t.shape[1], t.stride(0)
+    raise ValueError(f"expected NHWC or [rows, c] with contiguous channels, got {tuple(t.shape)} {t.stride()}")
+
+
+# ---------------------------------------------------------------------------------------- conv / linear
+@dataclass(frozen=True)
+class ConvCfg:
+    kh: int
+    kw: int
+    stride: int = 1
+    pad: int = 0
+    up2: bool = False
+    pixel_shuffle: bool = False
+    act: int = NONE
+    slope: float = 0.0
+    out_f32: bool = False
+    key: Optional[str] = None  # cache key of a frozen layer's packed weights (see TrainOps)
+
+
+class PackCache:
+    """Packed forward / dgrad weights of FROZEN layers (packed once); trainable layers repack per step."""
+
+    def __init__(self):
+        self.fwd, self.dgrad = {}, {}
+
+    def clear(self):
+        self.fwd.clear()
+        self.dgrad.clear()
+
+
+PACKS = PackCache()
+
+
+def _pack_fwd(weight: torch.Tensor, bias, cfg: ConvCfg, dtype, frozen: bool) -> ops.ConvParams:
+    key = (cfg.key, cfg.stride, cfg.pad, dtype)
+    if frozen and cfg.key is not None and key in PACKS.fwd:
+        return PACKS.fwd[key]
+    p = ops.ConvParams.pack(weight.detach(), None if bias is None else bias.detach(), stride=cfg.stride,
+                            pad=cfg.pad, dtype=dtype)
+    if frozen and cfg.key is not None:
+        PACKS.fwd[key] = p
+    return p
+
+
+def _pack_dgrad(weight: torch.Tensor, dtype, frozen: bool, key) -> tuple:
+    ck = (key, dtype)
+    if frozen and key is not None and ck in PACKS.dgrad:
+        return PACKS.dgrad[ck]
+    w = weight.detach()
+    if w.dim() == 2:
+        w = w[:, :, None, None]
+    w = w.contiguous()
+    cout, cin, kh, kw = w.shape
+    wld = -(-(kh * kw * cout) // 64) * 64
+    packed = torch.empty((cin, wld), dtype=dtype, device=w.device)
+    call("rdeic_pack_conv_weight_dgrad", w.data_ptr(), cout, cin, kh, kw, packed.data_ptr(), wld,
+         int(dtype == torch.bfloat16), _sp())
+    r = (packed, wld)
+    if frozen and key is not None:
+        PACKS.dgrad[ck] = r
+    return r
+
+
+def conv_dgrad(dz: torch.Tensor, weight: torch.Tensor, cfg: ConvCfg, in_hw, frozen: bool) -> torch.Tensor:
+    """Input gradient of a conv whose output gradient (after act / unshuffle) is dz [n, ho, wo, cout]."""
+    cout, cin = weight.shape[0], weight.shape[1]
+    packed, wld = _pack_dgrad(weight, dz.dtype, frozen, cfg.key)
+    p = ops.ConvParams(packed, wld, None, cin, cout, cfg.kh, cfg.kw, 1, cfg.kh - 1 - cfg.pad)
+    n = dz.shape[0]
+    h, w = in_hw
+    hi, wi = (2 * h, 2 * w) if cfg.up2 else (h, w)
+    src = dz
+    if cfg.stride == 2:
+        if hi != 2 * dz.shape[1] or wi != 2 * dz.shape[2]:
+            raise ValueError("stride-2 conv backward needs an even input size")
+        src = torch.empty((n, hi, wi, cout), dtype=dz.dtype, device=dz.device)
+        call("rdeic_zero_insert2", dz.data_ptr(), n, dz.shape[1], dz.shape[2], cout, ops.pix_ld(dz), src.data_ptr(),
+             cout, _dt(dz), _sp())
+    elif cfg.stride != 1:
+        raise ValueError("conv backward supports stride 1 and 2")
+    d_in = ops.conv2d(src, p, out_hw=(hi, wi))
+    if cfg.up2:
+        dx = torch.empty((n, h, w, cin), dtype=dz.dtype, device=dz.device)
+        call("rdeic_sum_pool2", d_in.data_ptr(), n, h, w, cin, cin, dx.data_ptr(), cin, _dt(dz), _sp())
+        return dx
+    return d_in
+
+
+def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, cfg: ConvCfg, cout: int, cin: int, out=None) -> torch.Tensor:
+    """fp32 [cout, cin, kh, kw] = dz^T . im2col(x) (split-K over pixels, fixed-order reduction)."""
+    n, ho, wo, _ = dz.shape
+    P = n * ho * wo
+    K = cfg.kh * cfg.kw * cin
+    ldz = ops.pix_ld(dz)
+    if cfg.kh == 1 and cfg.kw == 1 and cfg.stride == 1 and not cfg.up2 and cfg.pad == 0:
+        cols, b_sk = x, ops.pix_ld(x)
+    else:
+        cols = torch.empty((P, K), dtype=x.dtype, device=x.device)
+        call("rdeic_im2col", x.data_ptr(), x.shape[0], x.shape[1], x.shape[2], cin, ops.pix_ld(x), cfg.kh, cfg.kw,
+             cfg.stride, cfg.pad, cfg.pad, ho, wo, int(cfg.up2), cols.data_ptr(), K, _dt(x), _sp())
+        b_sk = K
+    tiles = -(-cout // 64) * -(-K // 64)
+    splits = max(1, min(-(-1024 // tiles), -(-P // 256), 64))
+    ks = -(-P // splits)
+    ks = -(-ks // 32) * 32
+    splits = -(-P // ks)
+    part = torch.empty((splits, cout, K), dtype=torch.float32, device=x.device)
+    gemm(dz, 0, 1, ldz, cols, 0, b_sk, 1, part, 0, K, m=cout, n=K, k=P, batch=splits, c_bs=(cout * K, 0), ksplit=ks)
+    if out is None:
+        out = torch.empty((cout, cin, cfg.kh, cfg.kw), dtype=torch.float32, device=x.device)
+    call("rdeic_wgrad_finalize", part.data_ptr(), splits, cout, cin, cfg.kh, cfg.kw, out.data_ptr(), 0, _sp())
+    return out
+
+
+def _conv_forward(x, weight, bias, emb, res, cfg: ConvCfg):
+    """(out, z): z = conv(x) + bias + emb (pre-activation, kept only when cfg.act != NONE)."""
+    frozen = not weight.requires_grad
+    p = _pack_fwd(weight, bias, cfg, x.dtype, frozen)
+    if p.cin != x.shape[3]:
+        raise ValueError(f"conv expects {p.cin} input channels, got {x.shape[3]}")
+    fused_res = res if cfg.act == NONE else None
+    z = ops.conv2d(x, p, up2=cfg.up2, emb=emb, res=fused_res, out_f32=cfg.out_f32, pixel_shuffle=cfg.pixel_shuffle)
+    if cfg.act == NONE:
+        return z, None
+    rows, c, ldz = _rows_view(z)
+    out = torch.empty_like(z)
+    r_ld = 0
+    if res is not None:
+        if res.shape != z.shape or res.dtype != z.dtype:
+            raise ValueError("residual must match the conv output")
+        r_ld = _rows_view(res)[2]
+    call("rdeic_act_fwd", z.data_ptr(), rows, c, ldz, None if res is None else res.data_ptr(), r_ld, cfg.act,
+         float(cfg.slope), out.data_ptr(), c, _dt(z), _sp())
+    return out, z
+
+
+def _conv_backward(x, weight, z, dout, cfg: ConvCfg, in_hw, need_x, need_w, need_b, need_emb):
+    """(dx, dw, db, demb) of _conv_forward given the output gradient (dres = dout)."""
+    dz = dout
+    if cfg.act != NONE:
+        rows, c, ldz = _rows_view(z)
+        dz = torch.empty_like(z)
+        call("rdeic_act_bwd", dout.data_ptr(), _rows_view(dout)[2], z.data_ptr(), ldz, rows, c, cfg.act,
+             float(cfg.slope), dz.data_ptr(), c, _dt(z), _sp())
+    if cfg.pixel_shuffle:
+        n, H2, W2, c = dz.shape
+        u = torch.empty((n, H2 // 2, W2 // 2, 4 * c), dtype=dz.dtype, device=dz.device)
+        call("rdeic_pixel_unshuffle2", dz.data_ptr(), n, H2 // 2, W2 // 2, c, ops.pix_ld(dz), u.data_ptr(), 4 * c,
+             _dt(dz), _sp())
+        dz = u
+    cout, cin = weight.shape[0], weight.shape[1]
+    if dz.dtype != x.dtype:  # fp32 output of a bf16 conv: gradients flow back in the compute dtype
+        dz = ops.cast(dz.contiguous(), x.dtype)
+    elif ops.pix_ld(dz) != cout:
+        dz = dz.contiguous()
+    n, ho, wo, _ = dz.shape
+    dx = dw = db = demb = None
+    if need_x:
+        dx = conv_dgrad(dz, weight, cfg, in_hw, frozen=not weight.requires_grad)
+    if need_w:
+        dw = conv_wgrad(x, dz, cfg, cout, cin).view(weight.shape)
+    if need_b:
+        db = col_sum(dz, n * ho * wo, cout, cout).view(cout)
+    if need_emb:
+        demb = col_sum(dz, n * ho * wo, cout, cout, groups=n)
+    return dx, dw, db, demb
+
+
+class Conv2dFn(torch.autograd.Function):
+    """out = act(conv(x) + bias + emb[img]) + res   (NHWC; PixelShuffle(2) after the conv when set)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, emb, res, cfg: ConvCfg):
+        out, z = _conv_forward(x, weight, bias, emb, res, cfg)
+        ctx.cfg = cfg
+        ctx.flags = (emb is not None, res is not None, bias is not None)
+        ctx.in_hw = (x.shape[1], x.shape[2])
+        ctx.save_for_backward(x, weight, z)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, weight, z = ctx.saved_tensors
+        has_emb, has_res, has_bias = ctx.flags
+        dout = dout.contiguous()
+        nig = ctx.needs_input_grad
+        dx, dw, db, demb = _conv_backward(x, weight, z, dout, ctx.cfg, ctx.in_hw, nig[0], nig[1],
+                                          has_bias and nig[2], has_emb and nig[3])
+        return dx, dw, db, demb, (dout if has_res else None), None
+
+
+def conv2d(x, weight, bias=None, *, emb=None, res=None, cfg: ConvCfg):
+    return Conv2dFn.apply(x, weight, bias, emb, res, cfg)
+
+
+def _tok4(t: torch.Tensor) -> torch.Tensor:
+    rows, c = t.shape
+    return t.as_strided((1, rows, 1, c), (rows * t.stride(0), t.stride(0), t.stride(0), 1))
+
+
+class LinearFn(torch.autograd.Function):
+    """Token-wise nn.Linear over [rows, cin] (row stride allowed) on the 1x1-conv kernels;
+    out = x W^T + b (+ res)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, res, cfg: ConvCfg):
+        rows = x.shape[0]
+        out, _ = _conv_forward(_tok4(x), weight, bias, None, None if res is None else _tok4(res), cfg)
+        ctx.cfg = cfg
+        ctx.flags = (res is not None, bias is not None)
+        ctx.save_for_backward(x, weight)
+        return out.view(rows, weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, weight = ctx.saved_tensors
+        has_res, has_bias = ctx.flags
+        dout = dout.contiguous()
+        rows = x.shape[0]
+        nig = ctx.needs_input_grad
+        dx, dw, db, _ = _conv_backward(_tok4(x), weight, None, _tok4(dout), ctx.cfg, (rows, 1), nig[0], nig[1],
+                                       has_bias and nig[2], False)
+        if dx is not None:
+            dx = dx.view(rows, weight.shape[1])
+        return dx, dw, db, (dout if has_res else None), None
+
+
+def linear(x2d: torch.Tensor, weight, bias=None, *, res=None, key=None, out_f32=False):
+    return LinearFn.apply(x2d, weight, bias, res, ConvCfg(1, 1, key=key, out_f32=out_f32))
+
+
+class CastFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return ops.cast(x, dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.cast(g.contiguous(), ctx.src), None
+
+
+def cast(x: torch.Tensor, dtype) -> torch.Tensor:
+    return x if x.dtype == dtype else CastFn.apply(x, dtype)
+
+
+class ActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, act: int, slope: float):
+        z = z.contiguous()
+        out = torch.empty_like(z)
+        c = z.shape[-1]
+        call("rdeic_act_fwd", z.data_ptr(), z.numel() // c, c, c, None, 0, act, float(slope), out.data_ptr(), c,
+             _dt(z), _sp())
+        ctx.act, ctx.slope = act, slope
+        ctx.save_for_backward(z)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (z,) = ctx.saved_tensors
+        g = g.contiguous()
+        dz = torch.empty_like(z)
+        c = z.shape[-1]
+        call("rdeic_act_bwd", g.data_ptr(), c, z.data_ptr(), c, z.numel() // c, c, ctx.act, float(ctx.slope),
+             dz.data_ptr(), c, _dt(z), _sp())
+        return dz, None, None
+
+
+def act(z, kind: int, slope: float = 0.0):
+    return ActFn.apply(z, kind, slope)
+
+
+# ------------------------------------------------------------------------------------------- norms
+class GroupNormFn(torch.autograd.Function):
+    """y = silu?(GroupNorm(x)) over NHWC x (GroupNorm32 / GroupNorm_leq32 / Normalize + SiLU)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool):
+        n, h, w, c = x.shape
+        hw = h * w
+        ld = ops.pix_ld(x)
+        mr = torch.empty((n, groups, 2), dtype=torch.float32, device=x.device)
+        ab = torch.empty((n, c, 2), dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(_lib.load().rdeic_gn_train_ws_doubles(n, hw, c)), dtype=torch.float64, device=x.device)
+        call("rdeic_gn_train_fwd", x.data_ptr(), ld, n, hw, c, groups, float(eps), gamma.data_ptr(), beta.data_ptr(),
+             mr.data_ptr(), ab.data_ptr(), ws.data_ptr(), _dt(x), _sp())
+        y = ops.group_norm_apply(x, ab, silu)
+        ctx.groups, ctx.silu = groups, silu
+        ctx.save_for_backward(x, gamma, beta, mr)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, mr = ctx.saved_tensors
+        dy = dy.contiguous()
+        n, h, w, c = x.shape
+        hw = h * w
+        dx = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)
+        want = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dg = torch.empty(c, dtype=torch.float32, device=x.device) if want else None
+        dbt = torch.empty(c, dtype=torch.float32, device=x.device) if want else None
+        ws = torch.empty(int(_lib.load().rdeic_gn_train_ws_doubles(n, hw, c)), dtype=torch.float64, device=x.device)
+        coef = torch.empty((n, ctx.groups, 2), dtype=torch.float32, device=x.device)
+        call("rdeic_gn_train_bwd", x.data_ptr(), ops.pix_ld(x), dy.data_ptr(), c, n, hw, c, ctx.groups, mr.data_ptr(),
+             gamma.data_ptr(), beta.data_ptr(), int(ctx.silu), dx.data_ptr(), c,
+             None if dg is None else dg.data_ptr(), None if dbt is None else dbt.data_ptr(), 0, ws.data_ptr(),
+             coef.data_ptr(), _dt(x), _sp())
+        return dx, dg, dbt, None, None, None
+
+
+def group_norm(x, gamma, beta, groups: int, eps: float, silu: bool):
+    return GroupNormFn.apply(x, gamma, beta, groups, eps, silu)
+
+
+class LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps: float):
+        rows, c = x.shape
+        y = torch.empty((rows, c), dtype=x.dtype, device=x.device)
+        call("rdeic_layernorm", x.data_ptr(), rows, c, x.stride(0), gamma.data_ptr(), beta.data_ptr(), float(eps),
+             y.data_ptr(), c, _dt(x), _sp())
+        ctx.eps = eps
+        ctx.save_for_backward(x, gamma)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, c = x.shape
+        dx = torch.empty((rows, c), dtype=x.dtype, device=x.device)
+        want = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dg = db = ws = None
+        nws = 0
+        if want:
+            dg = torch.empty(c, dtype=torch.float32, device=x.device)
+            db = torch.empty(c, dtype=torch.float32, device=x.device)
+            nws = int(_lib.load().rdeic_layernorm_bwd_ws_floats(rows, c))
+            ws = torch.empty(nws, dtype=torch.float32, device=x.device)
+        call("rdeic_layernorm_bwd", x.data_ptr(), x.stride(0), rows, c, gamma.data_ptr(), float(ctx.eps), dy.data_ptr(),
+             c, dx.data_ptr(), c, None if dg is None else dg.data_ptr(), None if db is None else db.data_ptr(), 0,
+             None if ws is None else ws.data_ptr(), nws, _dt(x), _sp())
+        return dx, dg, db, None
+
+
+def layer_norm(x, gamma, beta, eps: float = 1e-5):
+    return LayerNormFn.apply(x, gamma, beta, eps)
+
+
+# --------------------------------------------------------------------------------------- attention
+class AttentionFn(torch.autograd.Function):
+    """softmax(Q K^T * scale) V per (image, head) over 'b n (h d)' token tensors (CrossAttention.forward,
+    attention.py:171-203), materialised: P is kept for the backward."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, batch: int, heads: int, scale: float):
+        Lq = q.shape[0] // batch
+        Lk = k.shape[0] // batch
+        dh = q.shape[1] // heads
+        dev, dt = q.device, q.dtype
+        s = torch.empty((batch, heads, Lq, Lk), dtype=torch.float32, device=dev)
+        ldq, ldk, ldv = q.stride(0), k.stride(0), v.stride(0)
+        gemm(q, 0, ldq, 1, k, 0, 1, ldk, s, 0, Lk, m=Lq, n=Lk, k=dh, batch=batch * heads, nb2=heads,
+             a_bs=(Lq * ldq, dh), b_bs=(Lk * ldk, dh), c_bs=(heads * Lq * Lk, Lq * Lk))
+        p = torch.empty((batch, heads, Lq, Lk), dtype=dt, device=dev)
+        call("rdeic_softmax_rows", s.data_ptr(), batch * heads * Lq, Lk, float(scale), p.data_ptr(), _dt(q), _sp())
+        del s
+        o = torch.empty((batch * Lq, heads * dh), dtype=dt, device=dev)
+        gemm(p, 0, Lk, 1, v, 0, ldv, 1, o, 0, heads * dh, m=Lq, n=dh, k=Lk, batch=batch * heads, nb2=heads,
+             a_bs=(heads * Lq * Lk, Lq * Lk), b_bs=(Lk * ldv, dh), c_bs=(Lq * heads * dh, dh))
+        ctx.dims = (batch, heads, Lq, Lk, dh, scale)
+        ctx.save_for_backward(q, k, v, p)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, p = ctx.saved_tensors
+        batch, heads, Lq, Lk, dh, scale = ctx.dims
+        do = do.contiguous()
+        dev, dt = q.device, q.dtype
+        ldq, ldk, ldv, ldo = q.stride(0), k.stride(0), v.stride(0), do.stride(0)
+        nb = batch * heads
+        dp = torch.empty((batch, heads, Lq, Lk), dtype=torch.float32, device=dev)
+        gemm(do, 0, ldo, 1, v, 0, 1, ldv, dp, 0, Lk, m=Lq, n=Lk, k=dh, batch=nb, nb2=heads,
+             a_bs=(Lq * ldo, dh), b_bs=(Lk * ldv, dh), c_bs=(heads * Lq * Lk, Lq * Lk))
+        ds = torch.empty((batch, heads, Lq, Lk), dtype=dt, device=dev)
+        call("rdeic_softmax_bwd_rows", p.data_ptr(), dp.data_ptr(), nb * Lq, Lk, float(scale), ds.data_ptr(), _dt(q),
+             _sp())
+        del dp
+        pl = (heads * Lq * Lk, Lq * Lk)
+        dq = dk = dv = None
+        if ctx.needs_input_grad[0]:
+            dq = torch.empty((batch * Lq, heads * dh), dtype=dt, device=dev)
+            gemm(ds, 0, Lk, 1, k, 0, ldk, 1, dq, 0, heads * dh, m=Lq, n=dh, k=Lk, batch=nb, nb2=heads, a_bs=pl,
+                 b_bs=(Lk * ldk, dh), c_bs=(Lq * heads * dh, dh))
+        if ctx.needs_input_grad[1]:
+            dk = torch.empty((batch * Lk, heads * dh), dtype=dt, device=dev)
+            gemm(ds, 0, 1, Lk, q, 0, ldq, 1, dk, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=nb, nb2=heads, a_bs=pl,
+                 b_bs=(Lq * ldq, dh), c_bs=(Lk * heads * dh, dh))
+        if ctx.needs_input_grad[2]:
+            dv = torch.empty((batch * Lk, heads * dh), dtype=dt, device=dev)
+            gemm(p, 0, 1, Lk, do, 0, ldo, 1, dv, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=nb, nb2=heads, a_bs=pl,
+                 b_bs=(Lq * ldo, dh), c_bs=(Lk * heads * dh, dh))
+        return dq, dk, dv, None, None, None
+
+
+def attention(q, k, v, batch: int, heads: int, scale: float):
+    return AttentionFn.apply(q, k, v, batch, heads, scale)
+
+
+class GegluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        rows, c2 = x.shape
+        c = c2 // 2
+        out = torch.empty((rows, c), dtype=x.dtype, device=x.device)
+        call("rdeic_geglu", x.data_ptr(), rows, c, x.stride(0), out.data_ptr(), c, _dt(x), _sp())
+        ctx.save_for_backward(x)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, c2 = x.shape
+        dx = torch.empty((rows, c2), dtype=x.dtype, device=x.device)
+        call("rdeic_geglu_bwd", x.data_ptr(), x.stride(0), rows, c2 // 2, dy.data_ptr(), c2 // 2, dx.data_ptr(), c2,
+             _dt(x), _sp())
+        return dx
+
+
+def geglu(x):
+    return GegluFn.apply(x)
+
+
+# ------------------------------------------------------------------------- checkerboard entropy model
+class CkbdMaskFn(torch.autograd.Function):
+    """x at anchor (which=1) / non-anchor (which=0) positions, 0 elsewhere (utils/ckbd.py:33-45)."""
+
+    @staticmethod
+    def forward(ctx, x, which: int):
+        n, h, w, c = x.shape
+        out = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)
+        call("rdeic_ckbd_mask", x.data_ptr(), ops.pix_ld(x), n, h, w, c, which, out.data_ptr(), c, _dt(x), _sp())
+        ctx.which = which
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return CkbdMaskFn.apply(g.contiguous(), ctx.which), None
+
+
+class CkbdAnchorFn(torch.autograd.Function):
+    """slice_anchor_hat = quantize_ste(ckbd_anchor(y) - ckbd_anchor(mu_a)) + ckbd_anchor(mu_a)
+    (compression.py:86-89): value round(y - mu) + mu at anchors; gradient to y only (STE), none to mu."""
+
+    @staticmethod
+    def forward(ctx, y, pa):
+        n, h, w, c = y.shape
+        out = torch.empty((n, h, w, c), dtype=y.dtype, device=y.device)
+        call("rdeic_ckbd_train_anchor", y.data_ptr(), ops.pix_ld(y), pa.data_ptr(), ops.pix_ld(pa), n, h, w, c,
+             out.data_ptr(), c, _dt(y), _sp())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return CkbdMaskFn.apply(g.contiguous(), 1), None
+
+
+class CkbdLikFn(torch.autograd.Function):
+    """One slice's GaussianConditional likelihoods (noise mode -> S = sum ln lik, dequantize mode ->
+    qS, no gradient) and the non-anchor half of y_hat (quantize_ste), compression.py:94-106."""
+
+    @staticmethod
+    def forward(ctx, y, pa, pn, noise):
+        n, h, w, c = y.shape
+        non = torch.empty((n, h, w, c), dtype=y.dtype, device=y.device)
+        nws = int(_lib.load().rdeic_ckbd_train_ws_doubles(n, h, w, c))
+        ws = torch.empty(nws, dtype=torch.float64, device=y.device)
+        out2 = torch.empty(2, dtype=torch.float32, device=y.device)
+        call("rdeic_ckbd_train_lik", y.data_ptr(), ops.pix_ld(y), pa.data_ptr(), ops.pix_ld(pa), pn.data_ptr(),
+             ops.pix_ld(pn), noise.data_ptr(), n, h, w, c, non.data_ptr(), c, ws.data_ptr(), out2.data_ptr(), _dt(y),
+             _sp())
+        ctx.save_for_backward(y, pa, pn, noise)
+        S, qS = out2[0:1].clone(), out2[1:2].clone()
+        ctx.mark_non_differentiable(qS)
+        return S, qS, non
+
+    @staticmethod
+    def backward(ctx, gS, gq, gnon):
+        y, pa, pn, noise = ctx.saved_tensors
+        n, h, w, c = y.shape
+        dy = torch.empty((n, h, w, c), dtype=y.dtype, device=y.device)
+        dpa = torch.empty((n, h, w, 2 * c), dtype=y.dtype, device=y.device)
+        dpn = torch.empty((n, h, w, 2 * c), dtype=y.dtype, device=y.device)
+        gS = gS.to(torch.float32).contiguous()
+        gnon = None if gnon is None else gnon.contiguous()
+        call("rdeic_ckbd_train_lik_bwd", y.data_ptr(), ops.pix_ld(y), pa.data_ptr(), ops.pix_ld(pa), pn.data_ptr(),
+             ops.pix_ld(pn), noise.data_ptr(), n, h, w, c, gS.data_ptr(), None if gnon is None else gnon.data_ptr(), c,
+             dy.data_ptr(), c, dpa.data_ptr(), 2 * c, dpn.data_ptr(), 2 * c, _dt(y), _sp())
+        return dy, dpa, dpn, None
+
+
+# ------------------------------------------------------------------------------------ vector quantiser
+class VQTrainFn(torch.autograd.Function):
+    """VectorQuantiser.forward in training mode (compression_modules.py:228-307): nearest code,
+    commitment loss, contrastive loss, EMA usage and dead-code re-initialisation (in place on E and
+    embed_prob, like the reference's .data update). Returns (z_q straight-through, emb_loss[1])."""
+
+    @staticmethod
+    def forward(ctx, z, E, embed_prob, beta: float, decay: float, temp: float):
+        B, hz, wz, D = z.shape
+        P = B * hz * wz
+        K = E.shape[0]
+        dev = z.device
+        zf = ops.cast(z.contiguous(), torch.float32).view(P, D)
+        Ed = E.detach()
+        dot = torch.empty((P, K), dtype=torch.float32, device=dev)
+        gemm(zf, 0, D, 1, Ed, 0, 1, D, dot, 0, K, m=P, n=K, k=D)
+        zn = torch.empty(P, dtype=torch.float32, device=dev)
+        en = torch.empty(K, dtype=torch.float32, device=dev)
+        call("rdeic_row_sqnorm", zf.data_ptr(), P, D, D, zn.data_ptr(), 0, _sp())
+        call("rdeic_row_sqnorm", Ed.data_ptr(), K, D, D, en.data_ptr(), 0, _sp())
+        idx = torch.empty(P, dtype=torch.int32, device=dev)
+        call("rdeic_vq_argmin", dot.data_ptr(), zn.data_ptr(), en.data_ptr(), P, K, idx.data_ptr(), _sp())
+        zq = torch.empty((P, D), dtype=torch.float32, device=dev)
+        call("rdeic_gather_rows", Ed.data_ptr(), D, idx.data_ptr(), P, D, zq.data_ptr(), D, 0, _sp())
+        code_out = torch.empty((K, 2), dtype=torch.float32, device=dev)
+        dE_unit = torch.empty((K, D), dtype=torch.float32, device=dev)
+        loss3 = torch.empty(3, dtype=torch.float32, device=dev)
+        call("rdeic_vq_train", dot.data_ptr(), zn.data_ptr(), en.data_ptr(), zf.data_ptr(), idx.data_ptr(), P, K, D,
+             Ed.data_ptr(), embed_prob.data_ptr(), float(beta), float(decay), float(temp), code_out.data_ptr(),
+             dE_unit.data_ptr(), loss3.data_ptr(), _sp())
+        ctx.beta, ctx.shape, ctx.dt = beta, (B, hz, wz, D), z.dtype
+        ctx.save_for_backward(zf, zq, dE_unit)
+        ctx.idx = idx
+        out = ops.cast(zq, z.dtype).view(B, hz, wz, D)
+        return out, loss3[0:1].clone()
+
+    @staticmethod
+    def backward(ctx, dzq, dloss):
+        zf, zq, dE_unit = ctx.saved_tensors
+        B, hz, wz, D = ctx.shape
+        P = B * hz * wz
+        dloss = dloss.to(torch.float32).contiguous()
+        dz = torch.empty((B, hz, wz, D), dtype=ctx.dt, device=zf.device)
+        dzq = None if dzq is None else dzq.contiguous()
+        call("rdeic_vq_z_grad", zf.data_ptr(), zq.data_ptr(), None if dzq is None else dzq.data_ptr(), P * D,
+             dloss.data_ptr(), float(ctx.beta * 2.0 / (P * D)), dz.data_ptr(), _dt(dz), _sp())
+        dE = torch.empty_like(dE_unit)
+        call("rdeic_scale_dev", dE_unit.data_ptr(), dE_unit.numel(), dloss.data_ptr(), dE.data_ptr(), 0, _sp())
+        return dz, dE, None, None, None, None
+
+
+def adamw_(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
+           betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2) -> None:
+    """torch.optim.AdamW update of flat fp32 buffers in place (configure_optimizers, rdeic.py:763-772)."""
+    for t in (p, g, m, v):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("adamw_ expects contiguous fp32 buffers")
+    call("rdeic_adamw", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), float(lr), float(betas[0]),
+         float(betas[1]), float(eps), float(weight_decay), int(step), _sp())
+
+
+def bpp_from_sum(S: torch.Tensor, num_pixels: int) -> torch.Tensor:
+    """sum(log(lik)) / (-ln 2 * num_pixels)  (model/rdeic.py:684)."""
+    return S / (-math.log(2) * num_pixels)

@@ -79,3 +79,79 @@ def barrier(device=None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+class GradBuckets:
+    """DDP gradient all-reduce of the fine-tune step (config 5; the reference's PL `accelerator: ddp`,
+    configs/finetune_ood.yaml:28-30) over ONE flat fp32 gradient buffer.
+
+    The buffer is cut into buckets of ~bucket_bytes, from its END: parameters are laid out in
+    declaration (forward) order and the backward produces the last layers' gradients first. Each
+    parameter's post-accumulate-grad hook counts down its bucket; a bucket whose gradients are all
+    accumulated is all-reduced asynchronously right away (RCCL overlaps it with the rest of the
+    backward), and finish() launches any bucket that got no gradient this step (in bucket order, the
+    same on every rank), waits, and averages. xGMI rings are per-link bound (7 links x ~153 GB/s):
+    a few tens of MB per bucket keeps each collective long enough to run near link rate."""
+
+    def __init__(self, grad_flat: torch.Tensor, params, bucket_bytes: int = 32 << 20, group=None):
+        """params: [(leaf tensor, offset, numel)] in the buffer's layout order."""
+        self.grad, self.group = grad_flat, group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        cap = max(1, bucket_bytes // grad_flat.element_size())
+        self.buckets = []          # [lo, hi) element ranges of the flat buffer, launch order
+        self.owner = {}
+        self.count = []
+        cur_hi, cur_lo, members = None, None, 0
+        for p, off, n in reversed(list(params)):
+            if cur_hi is None:
+                cur_hi = off + n
+            cur_lo = off
+            self.owner[id(p)] = len(self.buckets)
+            members += 1
+            if cur_hi - cur_lo >= cap:
+                self.buckets.append((cur_lo, cur_hi))
+                self.count.append(members)
+                cur_hi, members = None, 0
+        if cur_hi is not None:
+            self.buckets.append((cur_lo, cur_hi))
+            self.count.append(members)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p, _, _ in params]
+        self.pending, self.handles, self.fired = [], {}, {}
+
+    def begin(self):
+        self.pending = list(self.count)
+        self.handles = {}
+        self.fired = {}
+
+    def _launch(self, b: int):
+        lo, hi = self.buckets[b]
+        if self.world > 1:
+            self.handles[b] = dist.all_reduce(self.grad[lo:hi], group=self.group, async_op=True)
+        else:
+            self.handles[b] = None
+
+    def _on_grad(self, p):
+        k = id(p)
+        self.fired[k] = self.fired.get(k, 0) + 1
+        if self.fired[k] > 1:
+            raise RuntimeError("a bucketed parameter received two gradient accumulations in one step")
+        b = self.owner[k]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch(b)
+
+    def finish(self):
+        for b in range(len(self.buckets)):
+            if b not in self.handles:
+                self._launch(b)
+        for b in range(len(self.buckets)):
+            h = self.handles[b]
+            if h is not None:
+                h.wait()
+        if self.world > 1:
+            self.grad.div_(self.world)
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -39,3 +39,18 @@ def relay_noise(shape, seed: int, steps: int):
     torch.randn(shape, generator=g)
     noise = torch.randn(shape, generator=g)
     return noise, torch.stack([torch.randn(shape, generator=g) for _ in range(steps)])
+
+
+def train_draws(batch: int, h: int, w: int, slice_ch, seed: int, used_timesteps: int = 300):
+    """The random draws of one adapter fine-tune step (model/rdeic.py:774-796, ddpm.py:665-672,
+    compressai GaussianConditional "noise" mode), from one CPU generator in the reference's order:
+    t ~ randint(0, used_timesteps) (rdeic.py:778), the posterior sample's randn
+    (distributions.py:36), one U(-0.5, 0.5) per entropy slice in slice order (NCHW [B, c, h/2, w/2]
+    of the 8x-down latent's y), then the p_losses randn (rdeic.py:795). h, w: latent size."""
+    g = torch.Generator().manual_seed(int(seed))
+    t = torch.randint(0, used_timesteps, (batch,), generator=g)
+    post_eps = torch.randn((batch, 4, h, w), generator=g)
+    hy, wy = h // 2, w // 2
+    slice_noise = [torch.rand((batch, c, hy, wy), generator=g) - 0.5 for c in slice_ch]
+    noise = torch.randn((batch, 4, h, w), generator=g)
+    return dict(t=t, post_eps=post_eps, slice_noise=slice_noise, noise=noise)

@@ -118,6 +118,14 @@ class AutoencoderKL:
     # ------------------------------------------------------------------ passes
     def encode_hc(self, x: torch.Tensor, out_mul: float = 1.0) -> torch.Tensor:
         """x: NHWC compute-dtype image in [-1, 1] ([B,H,W,3]); returns c * out_mul, [B,H/8,W/8,512]."""
+        return self._encode(x, out_mul, moments=False)
+
+    def encode_hc_moments(self, x: torch.Tensor, out_mul: float = 1.0):
+        """encode_hc + the posterior moments (autoencoder.py:91-95): (c * out_mul, moments fp32 NHWC
+        [B,H/8,W/8,8] = quant_conv(conv_out(c))) for the fine-tune step's x_start sample."""
+        return self._encode(x, out_mul, moments=True)
+
+    def _encode(self, x: torch.Tensor, out_mul: float, moments: bool):
         s = self.store
         e = self.prefix + "encoder."
         h = ops.conv2d(x, s.conv(e + "conv_in", cin_pad=x.shape[3] if x.shape[3] > 3 else None), stats=True)
@@ -132,7 +140,14 @@ class AutoencoderKL:
         h = self.attn(self.enc_mid[1], h)
         h = self.resnet(self.enc_mid[2], h)
         ab = ops.group_norm_ab(h, s.get(e + "norm_out.weight"), s.get(e + "norm_out.bias"), 32, GN_EPS)
-        return ops.group_norm_apply(h, ab, silu=True, out_mul=out_mul)
+        if not moments:
+            return ops.group_norm_apply(h, ab, silu=True, out_mul=out_mul)
+        c = ops.group_norm_apply(h, ab, silu=True)
+        hc = ops.conv2d(c, s.conv(e + "conv_out"), out_f32=True)
+        mom = ops.conv2d(hc, s.conv(self.prefix + "quant_conv", dtype=torch.float32))
+        if out_mul != 1.0:
+            c = ops.group_norm_apply(h, ab, silu=True, out_mul=out_mul)
+        return c, mom
 
     def decode(self, z: torch.Tensor, out_f32: bool = True) -> torch.Tensor:
         """z: compute-dtype NHWC [B,h,w,4] (already divided by the scale factor); returns NHWC [B,8h,8w,3]."""

@@ -95,10 +95,18 @@ def _install_stubs():
             assert mode == "symbols"
             return cr.quantize_symbols(inputs, means)
 
+        def forward(self, inputs, scales, means=None, training=None):
+            """Training-mode forward (oracle/train_ref.py restates compressai 1.2.4); the uniform
+            noise comes from train_ref.NOISE_QUEUE in call order."""
+            from oracle import train_ref
+            if training is None:
+                training = self.training
+            return train_ref.gaussian_forward(inputs, scales, means, training)
+
     em.EntropyModel = EntropyModel
     em.GaussianConditional = GaussianConditional
     ops = types.ModuleType("compressai.ops")
-    ops.quantize_ste = lambda x: (torch.round(x) - x).detach() + x
+    ops.quantize_ste = lambda x: (torch.round(x) - x).detach() + x  # compressai/ops/ops.py
     ans = types.ModuleType("compressai.ans")
     ans.BufferedRansEncoder = cr.RansEncoderRef
     ans.RansDecoder = cr.RansDecoderRef
