@@ -45,7 +45,7 @@ class LowerBoundFunction(torch.autograd.Function):
 
 
 def lower_bound(x: torch.Tensor, bound: float) -> torch.Tensor:
-    return LowerBoundFunction.apply(x, torch.tensor([float(bound)], dtype=x.dtype))
+    return LowerBoundFunction.apply(x, torch.tensor([float(bound)], dtype=x.dtype, device=x.device))
 
 
 def standardized_cumulative(x: torch.Tensor) -> torch.Tensor:

@@ -46,7 +46,7 @@ def step():
     params = {n: ft.flat[o:o + k].cpu() for n, (o, k) in ft.offsets.items()}
     fw = dict(x_start=x_start, h=h, **ft._last)
     fw = {k: v.detach().permute(0, 3, 1, 2).float().cpu().numpy() for k, v in fw.items()}
-    return dict(g=g, ft=ft, ld={k: float(v) for k, v in ld.items()}, grads=grads, params=params, fw=fw,
+    return dict(g=g, ft=ft, ld={k: float(v.detach()) for k, v in ld.items()}, grads=grads, params=params, fw=fw,
                 E_after_fwd=E_after_fwd, ep=ep)
 
 

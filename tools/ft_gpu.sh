@@ -1,0 +1,13 @@
+# Fine-tune step checks on one GPU: kernel-level backward tests, then the golden-step parity test.
+# usage: bash tools/ft_gpu.sh TAG   (stops after a crash / timeout; pytest failures (rc 1) continue)
+set -u
+O=gpurun_out/${1:-ft}
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_train_kernels_gpu.py -v --timeout 200 --timeout-method thread > $O/kern.log 2>&1
+rc=$?
+tail -8 $O/kern.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop: kernel tests rc=$rc"; exit $rc; fi
+timeout -k 10 400 python -u -m pytest tests/test_finetune_gpu.py -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?
+tail -30 $O/pytest.log
+exit $rc
