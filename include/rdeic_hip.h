@@ -302,6 +302,7 @@ int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row);
 #define RDEIC_PROF_ATTN_SMALL 2  /* rdeic_attention, head dim < 64 */
 #define RDEIC_PROF_GN_STATS 3    /* rdeic_groupnorm_stats: bytes read */
 #define RDEIC_PROF_GN_APPLY 4    /* rdeic_groupnorm_apply: bytes read + written */
+#define RDEIC_PROF_GEMM 5        /* rdeic_gemm_strided (training backward / attention): 2*M*N*K*batch FLOPs */
 int rdeic_prof_start(int32_t capacity, int32_t every);
 int rdeic_prof_stop(void);
 int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms);

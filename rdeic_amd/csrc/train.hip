@@ -16,6 +16,7 @@
 // Every reduction runs in a fixed order (no atomics): a step is bit-reproducible run to run.
 #include "common.h"
 #include "../../include/rdeic_hip.h"
+#include "prof.h"
 
 // the optimizer / loss arithmetic follows torch's separate roundings: no fma contraction
 #pragma clang fp contract(off)
@@ -916,6 +917,8 @@ extern "C" int rdeic_gemm_strided(const rdeic_gemm_desc* d, void* stream) {
   dim3 grid((d->n + GBN - 1) / GBN, (d->m + GBM - 1) / GBM, d->batch);
   if (d->batch > 65535) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  const double flops = 2.0 * d->m * d->n * (d->ksplit > 0 ? (double)d->k : (double)d->k * (d->batch / d->nb2)) * d->nb2;
+  ProfScope ps(s, RDEIC_PROF_GEMM, flops);
   if (d->dtype == 1)
     hipLaunchKernelGGL(gemm_strided_kernel<bf16>, grid, dim3(256), 0, s, g);
   else

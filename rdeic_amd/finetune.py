@@ -353,7 +353,21 @@ class FineTuner:
         elif sync_grads is not None:
             sync_grads(self.grad)
         self.optimizer_step()
+        if self.buckets is not None:
+            self.sync_codebook()
         return d
+
+    def sync_codebook(self, src: int = 0):
+        """Data-parallel replicas: VectorQuantiser.forward re-initialises dead codes in place from each
+        rank's OWN batch (compression_modules.py:272-296), which no gradient all-reduce covers (the
+        reference only ever trains on one GPU, finetune_ood.yaml:28-30). Keep the replicas identical by
+        taking rank `src`'s codebook and usage EMA after the step (16 MB broadcast)."""
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        o, k = self.offsets[self.m.preprocess_model.p + "quantize.embedding.weight"]
+        dist.broadcast(self.flat[o:o + k], src)
+        dist.broadcast(self.embed_prob, src)
 
 
 def nchw_draws_to_nhwc(dr: dict, device) -> dict:
