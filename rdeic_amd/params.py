@@ -101,6 +101,24 @@ class ParamStore:
             self._packed[key] = p
         return p
 
+    def conv_split_pad(self, prefix: str, c0: int, c0_pad: int, dtype=None) -> ops.ConvParams:
+        """A conv over cat(x [c0 ch], x2) packed for x zero-padded to c0_pad channels: input channels
+        [0, c0) stay, [c0, cin) move to [c0_pad, ...), the columns between are zero. Used for the
+        control branch's cat(x_t [4], hint [256]) input conv so both segments are 64-channel aligned
+        (LDS-DMA path) instead of the 260-channel register-staged path."""
+        dtype = dtype or self.compute_dtype
+        key = (prefix, "split_pad", c0, c0_pad, dtype)
+        p = self._packed.get(key)
+        if p is None:
+            w = self.t[prefix + ".weight"]
+            cout, cin, kh, kw = w.shape
+            wp = torch.zeros((cout, cin - c0 + c0_pad, kh, kw), dtype=w.dtype, device=w.device)
+            wp[:, :c0] = w[:, :c0]
+            wp[:, c0_pad:] = w[:, c0:]
+            p = ops.ConvParams.pack(wp, self.t.get(prefix + ".bias"), stride=1, pad=kh // 2, dtype=dtype)
+            self._packed[key] = p
+        return p
+
     def conv_geglu(self, prefix: str, dtype=None) -> ops.ConvParams:
         """GEGLU projection (attention.py:49-56, value = rows [0, c), gate = rows [c, 2c)) packed for the
         fused epilogue (ops.linear(geglu=True)): rows reordered in groups of 4 as (value 4j..4j+3,

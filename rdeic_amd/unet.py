@@ -300,6 +300,21 @@ class NoiseEstimator:
         self._freqs_cpu = torch.exp(-math.log(10000) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
         self._freqs = None
 
+    def _pad64(self, x: torch.Tensor) -> torch.Tensor:
+        """x [B,h,w,c<64] -> [B,h,w,64] with channels c.. zero (the pad buffer is zeroed once per shape;
+        only channels [0, c) are written per call, also under launch-plan replay)."""
+        B, H, W_, c = x.shape
+        key = (B, H, W_, x.dtype, ops.stream_ptr())
+        cache = self.__dict__.setdefault("_pad_cache", {})
+        buf = cache.get(key)
+        if buf is None:
+            buf = torch.zeros((B, H, W_, 64), dtype=x.dtype, device=x.device)
+            cache[key] = buf
+        xc = x.contiguous()
+        ops.call("rdeic_act_fwd", xc.data_ptr(), B * H * W_, c, c, None, 0, 0, 0.0, buf.data_ptr(), 64,
+                 ops.dt_code(x), ops.stream_ptr())
+        return buf
+
     def timestep_embedding(self, t: torch.Tensor) -> torch.Tensor:
         if self._freqs is None:
             self._freqs = self._freqs_cpu.to(t.device)
@@ -358,8 +373,15 @@ class NoiseEstimator:
         # each zero-conv add (next block, and the decoder's skip concat), the control features, the
         # last decoder block's output (the final norm)
         for i, (lb, lc) in enumerate(zip(self.base.input_blocks, self.ctrl.input_blocks)):
+            h_base0 = h_base
             h_base = self.base.run_layers(lb, h_base, emb_b, ctx_rows, Bc, Lc, stats_last=False)
-            h_ctr = self.ctrl.run_layers(lc, h_ctr, emb_c, ctx_rows, Bc, Lc, x2=ctr_x2)
+            if i == 0 and dt == torch.bfloat16 and len(lc) == 1 and isinstance(lc[0], Conv) and \
+                    h_base0.shape[3] % 64 and hint.shape[3] % 64 == 0:
+                # cat(x_t, hint): x_t zero-padded to 64 channels -> both segments take the LDS-DMA path
+                h_ctr = ops.conv2d(self._pad64(h_base0), s.conv_split_pad(lc[0].prefix, h_base0.shape[3], 64),
+                                   x2=hint, stats=True)
+            else:
+                h_ctr = self.ctrl.run_layers(lc, h_ctr, emb_c, ctx_rows, Bc, Lc, x2=ctr_x2)
             ctr_x2 = None
             h_base = ops.conv2d(h_ctr, s.conv(self.enc_zero[i], scale=sc), res=h_base, stats=True)
             hs_base.append(h_base)
