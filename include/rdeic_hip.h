@@ -412,6 +412,9 @@ int rdeic_scale_dev(const float* x, int64_t count, const float* s, float* y, int
 /* torch.optim.AdamW (decoupled weight decay) over flat fp32 buffers, step >= 1 */
 int rdeic_adamw(float* p, const float* g, float* m, float* v, int64_t count, float lr, float beta1, float beta2,
                 float eps, float weight_decay, int32_t step, void* stream);
+/* the same update with step_scalars = device [-lr / (1 - beta1^step), sqrt(1 - beta2^step)] (graph replay) */
+int rdeic_adamw_dev(float* p, const float* g, float* m, float* v, int64_t count, float lr, float beta1, float beta2,
+                    float eps, float weight_decay, const float* step_scalars, void* stream);
 
 #ifdef __cplusplus
 }

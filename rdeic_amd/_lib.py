@@ -161,6 +161,7 @@ PROTOTYPES = {
     "rdeic_vq_z_grad": (C.c_int, [_p, _p, _p, _i64, _p, _f, _p, _i32, _p]),
     "rdeic_scale_dev": (C.c_int, [_p, _i64, _p, _p, _i32, _p]),
     "rdeic_adamw": (C.c_int, [_p, _p, _p, _p, _i64, _f, _f, _f, _f, _f, _i32, _p]),
+    "rdeic_adamw_dev": (C.c_int, [_p, _p, _p, _p, _i64, _f, _f, _f, _f, _f, _p, _p]),
 }
 
 _lib = None

@@ -71,15 +71,41 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
   const int ar = a_kc ? (tid >> 2) : ((tid & 7) * 8), ak = a_kc ? ((tid & 3) * 8) : (tid >> 3);
   const int br = b_kc ? (tid >> 2) : ((tid & 7) * 8), bk = b_kc ? ((tid & 3) * 8) : (tid >> 3);
   T ra[8], rb[8];
-  auto load = [&](long k0) {
+  // 8 elements a thread stages per operand are contiguous in memory when the staged dimension has
+  // stride 1 (k for a_kc / b_kc, else m / n): one (bf16) or two (fp32) 16-byte loads when aligned and
+  // in bounds, element loads otherwise
+  const bool a_vec = a_kc || g.a_sm == 1, b_vec = b_kc || g.b_sn == 1;
+  auto load8 = [&](const T* base, long step, bool contiguous, int valid, T (&r)[8]) {
+    if (contiguous && valid == 8 && ((uintptr_t)base & 15) == 0) {
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(r) = *reinterpret_cast<const uint4*>(base);
+      } else {
+        reinterpret_cast<uint4*>(r)[0] = reinterpret_cast<const uint4*>(base)[0];
+        reinterpret_cast<uint4*>(r)[1] = reinterpret_cast<const uint4*>(base)[1];
+      }
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int mm = a_kc ? ar : ar + e;
-      const long kk = k0 + (a_kc ? ak + e : ak);
-      ra[e] = (m0 + mm < g.m && kk < klen) ? A[(long)(m0 + mm) * g.a_sm + kk * g.a_sk] : from_f32<T>(0.f);
-      const int nn = b_kc ? br : br + e;
-      const long kb = k0 + (b_kc ? bk + e : bk);
-      rb[e] = (n0 + nn < g.n && kb < klen) ? B[kb * g.b_sk + (long)(n0 + nn) * g.b_sn] : from_f32<T>(0.f);
+      for (int e = 0; e < 8; ++e) r[e] = e < valid ? base[e * step] : from_f32<T>(0.f);
+    }
+  };
+  auto load = [&](long k0) {
+    if (a_kc) {
+      const long kk = k0 + ak;
+      const int valid = (m0 + ar < g.m) ? (int)max(0L, min(8L, klen - kk)) : 0;
+      load8(A + (long)(m0 + ar) * g.a_sm + kk, 1, true, valid, ra);
+    } else {
+      const long kk = k0 + ak;
+      const int valid = kk < klen ? max(0, min(8, g.m - (m0 + ar))) : 0;
+      load8(A + (long)(m0 + ar) * g.a_sm + kk * g.a_sk, g.a_sm, a_vec, valid, ra);
+    }
+    if (b_kc) {
+      const long kb = k0 + bk;
+      const int valid = (n0 + br < g.n) ? (int)max(0L, min(8L, klen - kb)) : 0;
+      load8(B + kb + (long)(n0 + br) * g.b_sn, 1, true, valid, rb);
+    } else {
+      const long kb = k0 + bk;
+      const int valid = kb < klen ? max(0, min(8, g.n - (n0 + br))) : 0;
+      load8(B + kb * g.b_sk + (long)(n0 + br) * g.b_sn, g.b_sn, b_vec, valid, rb);
     }
   };
   f32x4 acc[2][2];
@@ -91,10 +117,21 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
   load(0);
   for (long k0 = 0; k0 < klen; k0 += GBK) {
     __syncthreads();
+    if (a_kc) {
+      if constexpr (sizeof(T) == 2) *reinterpret_cast<uint4*>(&As[ar][ak]) = *reinterpret_cast<const uint4*>(ra);
+      else { reinterpret_cast<uint4*>(&As[ar][ak])[0] = reinterpret_cast<const uint4*>(ra)[0];
+             reinterpret_cast<uint4*>(&As[ar][ak])[1] = reinterpret_cast<const uint4*>(ra)[1]; }
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (a_kc) As[ar][ak + e] = ra[e]; else As[ar + e][ak] = ra[e];
-      if (b_kc) Bs[br][bk + e] = rb[e]; else Bs[br + e][bk] = rb[e];
+      for (int e = 0; e < 8; ++e) As[ar + e][ak] = ra[e];
+    }
+    if (b_kc) {
+      if constexpr (sizeof(T) == 2) *reinterpret_cast<uint4*>(&Bs[br][bk]) = *reinterpret_cast<const uint4*>(rb);
+      else { reinterpret_cast<uint4*>(&Bs[br][bk])[0] = reinterpret_cast<const uint4*>(rb)[0];
+             reinterpret_cast<uint4*>(&Bs[br][bk])[1] = reinterpret_cast<const uint4*>(rb)[1]; }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Bs[br + e][bk] = rb[e];
     }
     __syncthreads();
     if (k0 + GBK < klen) load(k0 + GBK);
@@ -259,7 +296,7 @@ __global__ void wgrad_finalize_kernel(const float* __restrict__ part, int splits
 }
 
 // column sums: stage 1 per (group, row chunk), stage 2 over chunks in order
-constexpr int CS_ROWS = 256;
+constexpr int CS_ROWS = 32;  // rows per stage-1 block (B=1 training shapes: enough blocks to fill the chip)
 template <typename T>
 __global__ void col_sum_partial_kernel(const T* __restrict__ x, long rows_per_group, int c, int ld, int nchunk,
                                        float* __restrict__ ws) {
@@ -329,7 +366,7 @@ __global__ void act_bwd_kernel(const T* __restrict__ dy, int ldy, const T* __res
 // GroupNorm (training). Partials per (image, pixel chunk, channel) in fp64:
 //   MODE 0 (forward):  (sum x, sum x^2)
 //   MODE 1 (backward): (sum dY, sum dY * xhat), dY = dy * silu'(gamma*xhat + beta) (or dy)
-constexpr int GNT_CHUNK = 256;
+constexpr int GNT_CHUNK = 32;  // pixels per partial (grid = chunks x images x 256-channel blocks)
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gnt_partial_kernel(const T* __restrict__ x, int ldx, const T* __restrict__ dy,
                                                           int ldy, int hw, int c, int groups, int nchunk,
@@ -339,7 +376,9 @@ __global__ __launch_bounds__(256) void gnt_partial_kernel(const T* __restrict__ 
   const int img = blockIdx.y, chunk = blockIdx.x;
   const int p0 = chunk * GNT_CHUNK, p1 = min(hw, p0 + GNT_CHUNK);
   const int cpg = c / groups;
-  for (int ch = threadIdx.x; ch < c; ch += 256) {
+  {
+    const int ch = blockIdx.z * 256 + threadIdx.x;
+    if (ch >= c) return;
     double s1 = 0.0, s2 = 0.0;
     float mean = 0.f, rstd = 0.f, ga = 1.f, be = 0.f;
     if (MODE == 1) {
@@ -564,15 +603,26 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict_
   }
 }
 
-// sum over waves of the LayerNorm (dgamma, dbeta) partials
-__global__ void ln_param_grad_kernel(const float* __restrict__ part, long nwaves, int c, float* __restrict__ dgamma,
+// LayerNorm (dgamma, dbeta): the per-wave partials [nwaves][c][2] summed in 32-wave chunks (stage 1,
+// grid over chunks x channel blocks), then over the chunks in order (stage 2)
+constexpr int LN_CHUNK = 32;
+__global__ void ln_param_partial_kernel(const float* __restrict__ part, long nwaves, int c2, float* __restrict__ ws) {
+  const int col = blockIdx.x * 256 + threadIdx.x, chunk = blockIdx.y;
+  if (col >= c2) return;
+  const long w0 = (long)chunk * LN_CHUNK, w1 = min(nwaves, w0 + LN_CHUNK);
+  float sacc = 0.f;
+  for (long w = w0; w < w1; ++w) sacc += part[w * c2 + col];
+  ws[(long)chunk * c2 + col] = sacc;
+}
+
+__global__ void ln_param_grad_kernel(const float* __restrict__ ws, int nchunk, int c, float* __restrict__ dgamma,
                                      float* __restrict__ dbeta, int accumulate) {
   const int col = blockIdx.x * 256 + threadIdx.x;
   if (col >= c) return;
   float g = 0.f, b = 0.f;
-  for (long w = 0; w < nwaves; ++w) {
-    g += part[(w * c + col) * 2];
-    b += part[(w * c + col) * 2 + 1];
+  for (int q = 0; q < nchunk; ++q) {
+    g += ws[(long)q * 2 * c + 2 * col];
+    b += ws[(long)q * 2 * c + 2 * col + 1];
   }
   dgamma[col] = accumulate ? dgamma[col] + g : g;
   dbeta[col] = accumulate ? dbeta[col] + b : b;
@@ -856,11 +906,14 @@ __global__ __launch_bounds__(256) void vq_code_kernel(const float* __restrict__ 
 }
 
 // emb_loss = beta*mse + mse + mean_e CE_e, mse = sum_e sq_e / numel (one thread, fixed order)
-__global__ void vq_loss_kernel(const float* __restrict__ code_out, int K, float numel, float beta,
-                               float* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(256) void vq_loss_kernel(const float* __restrict__ code_out, int K, float numel,
+                                                      float beta, float* __restrict__ out) {
+  __shared__ double red[4];
   double ce = 0.0, sq = 0.0;
-  for (int e = 0; e < K; ++e) { ce += code_out[2 * e]; sq += code_out[2 * e + 1]; }
+  for (int e = threadIdx.x; e < K; e += 256) { ce += code_out[2 * e]; sq += code_out[2 * e + 1]; }
+  ce = block_sum_d(ce, red);
+  sq = block_sum_d(sq, red);
+  if (threadIdx.x != 0) return;
   const float mse = (float)(sq / numel);
   out[0] = (beta * mse + mse) + (float)(ce / K);
   out[1] = mse;
@@ -888,6 +941,24 @@ __global__ void scale_dev_kernel(const float* __restrict__ x, long count, const 
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, long count, float c_wd, float one_m_b1, float b2, float one_m_b2,
                              float bc2_sqrt, float neg_step, float eps) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < count; i += (long)gridDim.x * 256) {
+    const float gi = g[i];
+    const float pi = p[i] * c_wd;
+    const float mi = m[i] + one_m_b1 * (gi - m[i]);
+    const float vi = v[i] * b2 + one_m_b2 * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi + neg_step * mi / denom;
+  }
+}
+
+// as adamw_kernel, with the step-dependent scalars (-lr / bias_correction1, sqrt(bias_correction2))
+// read from device memory: a captured hipGraph replays the same launch every step
+__global__ void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                 float* __restrict__ v, long count, float c_wd, float one_m_b1, float b2,
+                                 float one_m_b2, const float* __restrict__ sc, float eps) {
+  const float neg_step = sc[0], bc2_sqrt = sc[1];
   for (long i = blockIdx.x * 256L + threadIdx.x; i < count; i += (long)gridDim.x * 256) {
     const float gi = g[i];
     const float pi = p[i] * c_wd;
@@ -1047,10 +1118,10 @@ extern "C" int rdeic_gn_train_fwd(const void* x, int32_t ldx, int32_t n, int32_t
   hipStream_t s = (hipStream_t)stream;
   const int nchunk = (hw + GNT_CHUNK - 1) / GNT_CHUNK;
   if (dtype == 1)
-    hipLaunchKernelGGL((gnt_partial_kernel<bf16, 0>), dim3(nchunk, n), dim3(256), 0, s, (const bf16*)x, ldx,
+    hipLaunchKernelGGL((gnt_partial_kernel<bf16, 0>), dim3(nchunk, n, (c + 255) / 256), dim3(256), 0, s, (const bf16*)x, ldx,
                        (const bf16*)nullptr, 0, hw, c, groups, nchunk, nullptr, nullptr, nullptr, 0, ws);
   else
-    hipLaunchKernelGGL((gnt_partial_kernel<float, 0>), dim3(nchunk, n), dim3(256), 0, s, (const float*)x, ldx,
+    hipLaunchKernelGGL((gnt_partial_kernel<float, 0>), dim3(nchunk, n, (c + 255) / 256), dim3(256), 0, s, (const float*)x, ldx,
                        (const float*)nullptr, 0, hw, c, groups, nchunk, nullptr, nullptr, nullptr, 0, ws);
   hipLaunchKernelGGL(gnt_fwd_finalize_kernel, dim3(groups, n), dim3(256), 0, s, ws, hw, c, groups, nchunk, eps, gamma,
                      beta, mr, ab);
@@ -1068,10 +1139,10 @@ extern "C" int rdeic_gn_train_bwd(const void* x, int32_t ldx, const void* dy, in
   double* part = ws;
   double* nc = ws + (size_t)n * nchunk * c * 2;
   if (dtype == 1)
-    hipLaunchKernelGGL((gnt_partial_kernel<bf16, 1>), dim3(nchunk, n), dim3(256), 0, s, (const bf16*)x, ldx,
+    hipLaunchKernelGGL((gnt_partial_kernel<bf16, 1>), dim3(nchunk, n, (c + 255) / 256), dim3(256), 0, s, (const bf16*)x, ldx,
                        (const bf16*)dy, ldy, hw, c, groups, nchunk, mr, gamma, beta, silu, part);
   else
-    hipLaunchKernelGGL((gnt_partial_kernel<float, 1>), dim3(nchunk, n), dim3(256), 0, s, (const float*)x, ldx,
+    hipLaunchKernelGGL((gnt_partial_kernel<float, 1>), dim3(nchunk, n, (c + 255) / 256), dim3(256), 0, s, (const float*)x, ldx,
                        (const float*)dy, ldy, hw, c, groups, nchunk, mr, gamma, beta, silu, part);
   hipLaunchKernelGGL(gnt_bwd_finalize_kernel, dim3(groups, n), dim3(256), 0, s, part, hw, c, groups, nchunk, gamma, nc,
                      coef);
@@ -1088,10 +1159,12 @@ extern "C" int rdeic_gn_train_bwd(const void* x, int32_t ldx, const void* dy, in
   return launch_status();
 }
 
+static long ln_bwd_blocks(long rows) { return std::min<long>((rows + 3) / 4, 256); }
+
 extern "C" size_t rdeic_layernorm_bwd_ws_floats(int64_t rows, int32_t c) {
   if (rows <= 0 || c <= 0) return 0;
-  const long blocks = std::min<long>((rows + 3) / 4, 1024);
-  return (size_t)blocks * 4 * c * 2;
+  const long nw = ln_bwd_blocks(rows) * 4;
+  return (size_t)nw * c * 2 + (size_t)((nw + LN_CHUNK - 1) / LN_CHUNK) * c * 2;
 }
 
 extern "C" int rdeic_layernorm_bwd(const void* x, int32_t ldx, int64_t rows, int32_t c, const float* gamma, float eps,
@@ -1101,16 +1174,21 @@ extern "C" int rdeic_layernorm_bwd(const void* x, int32_t ldx, int64_t rows, int
   const bool pg = dgamma && dbeta;
   if (pg && (!ws || ws_floats < rdeic_layernorm_bwd_ws_floats(rows, c))) return RDEIC_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
-  const int blocks = (int)std::min<long>((rows + 3) / 4, 1024);
+  const int blocks = (int)ln_bwd_blocks(rows);
   if (dtype == 1)
     hipLaunchKernelGGL(layernorm_bwd_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, ldx, (long)rows, c,
                        gamma, eps, (const bf16*)dy, ldy, (bf16*)dx, lddx, pg ? ws : nullptr);
   else
     hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, ldx, (long)rows, c,
                        gamma, eps, (const float*)dy, ldy, (float*)dx, lddx, pg ? ws : nullptr);
-  if (pg)
-    hipLaunchKernelGGL(ln_param_grad_kernel, dim3((c + 255) / 256), dim3(256), 0, s, ws, (long)blocks * 4, c, dgamma,
-                       dbeta, accumulate);
+  if (pg) {
+    const long nw = (long)blocks * 4;
+    const int nchunk = (int)((nw + LN_CHUNK - 1) / LN_CHUNK);
+    float* ws2 = ws + nw * c * 2;
+    hipLaunchKernelGGL(ln_param_partial_kernel, dim3((2 * c + 255) / 256, nchunk), dim3(256), 0, s, ws, nw, 2 * c, ws2);
+    hipLaunchKernelGGL(ln_param_grad_kernel, dim3((c + 255) / 256), dim3(256), 0, s, ws2, nchunk, c, dgamma, dbeta,
+                       accumulate);
+  }
   return launch_status();
 }
 
@@ -1223,7 +1301,7 @@ extern "C" int rdeic_vq_train(const float* dot, const float* zn, const float* en
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(vq_code_kernel, dim3(K), dim3(256), 0, s, dot, zn, en, z, idx, P, K, D, E, embed_prob, beta, decay,
                      temp, code_out, dE_unit);
-  hipLaunchKernelGGL(vq_loss_kernel, dim3(1), dim3(64), 0, s, code_out, K, (float)P * (float)D, beta, loss3);
+  hipLaunchKernelGGL(vq_loss_kernel, dim3(1), dim3(256), 0, s, code_out, K, (float)P * (float)D, beta, loss3);
   return launch_status();
 }
 
@@ -1256,5 +1334,14 @@ extern "C" int rdeic_adamw(float* p, const float* g, float* m, float* v, int64_t
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_1d(count)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)count,
                      (float)(1.0 - (double)lr * weight_decay), (float)(1.0 - (double)beta1), beta2,
                      (float)(1.0 - (double)beta2), (float)sqrt(bc2), (float)(-(double)lr / bc1), eps);
+  return launch_status();
+}
+
+extern "C" int rdeic_adamw_dev(float* p, const float* g, float* m, float* v, int64_t count, float lr, float beta1,
+                               float beta2, float eps, float weight_decay, const float* step_scalars, void* stream) {
+  if (!p || !g || !m || !v || !step_scalars || count <= 0) return RDEIC_EINVAL;
+  hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_1d(count)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)count,
+                     (float)(1.0 - (double)lr * weight_decay), (float)(1.0 - (double)beta1), beta2,
+                     (float)(1.0 - (double)beta2), step_scalars, eps);
   return launch_status();
 }

@@ -325,18 +325,34 @@ class FineTuner:
         loss = loss + cfg.l_guide_weight * loss_guide
         d = {"T/l_simple": loss_simple.mean(), "T/l_bpp": bpp[0], "T/q_bpp": q_bpp[0], "T/l_emb": emb_loss[0],
              "T/l_guide": loss_guide, "T/loss": loss}
-        self._last = dict(c_latent=c_latent, eps=eps, x_noisy=x_noisy, guide_hint=guide_hint)
+        # detached: holding the autograd graph past the step would keep the parameters' AccumulateGrad
+        # nodes (and their stream) alive into the next step / a graph capture
+        self._last = dict(c_latent=c_latent.detach(), eps=eps.detach(), x_noisy=x_noisy.detach(),
+                          guide_hint=guide_hint.detach())
         return loss, d
 
     def zero_grad(self):
         self.grad.zero_()
 
+    def adam_scalars(self, step: int) -> torch.Tensor:
+        """[-lr / (1 - beta1^step), sqrt(1 - beta2^step)] in Python doubles, as torch.optim.AdamW forms them."""
+        c = self.cfg
+        b1, b2 = c.betas
+        return torch.tensor([-c.learning_rate / (1 - b1 ** step), (1 - b2 ** step) ** 0.5], dtype=torch.float32)
+
+    def adamw_launch(self, sc_dev: torch.Tensor):
+        c = self.cfg
+        AG.call("rdeic_adamw_dev", self.flat.data_ptr(), self.grad.data_ptr(), self.exp_avg.data_ptr(),
+                self.exp_avg_sq.data_ptr(), self.flat.numel(), float(c.learning_rate), float(c.betas[0]),
+                float(c.betas[1]), float(c.eps), float(c.weight_decay), sc_dev.data_ptr(), ops.stream_ptr())
+
     def optimizer_step(self):
         """AdamW over the flat trainable buffer (torch.optim.AdamW defaults, lr from the config)."""
         self.step_count += 1
-        c = self.cfg
-        AG.adamw_(self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.step_count, c.learning_rate, c.betas,
-                  c.eps, c.weight_decay)
+        if getattr(self, "_sc", None) is None:
+            self._sc = torch.zeros(2, dtype=torch.float32, device=self.flat.device)
+        self._sc.copy_(self.adam_scalars(self.step_count), non_blocking=True)
+        self.adamw_launch(self._sc)
 
     def training_step(self, img_u8, ctx, draws: dict, sync_grads=None):
         """One step: forward, backward, (all-reduce), AdamW. img_u8 uint8 [B,H,W,3] on the device;
@@ -346,8 +362,11 @@ class FineTuner:
         x_start, h = self.get_first_stage(img_u8, draws["post_eps"])
         if self.buckets is not None:
             self.buckets.begin()
-        loss, d = self.losses(x_start, h, ctx, draws["t"], draws["noise"], draws["slice_noise"])
-        loss.backward()
+        # training needs no batch invariance anywhere: small-M / large-K convs (B=1 UNet levels, input
+        # gradients) may split K (deterministic, fixed-order reduction)
+        with ops.splitk_allowed():
+            loss, d = self.losses(x_start, h, ctx, draws["t"], draws["noise"], draws["slice_noise"])
+            loss.backward()
         if self.buckets is not None:
             self.buckets.finish()
         elif sync_grads is not None:
@@ -355,7 +374,7 @@ class FineTuner:
         self.optimizer_step()
         if self.buckets is not None:
             self.sync_codebook()
-        return d
+        return {k: v.detach() for k, v in d.items()}
 
     def sync_codebook(self, src: int = 0):
         """Data-parallel replicas: VectorQuantiser.forward re-initialises dead codes in place from each
@@ -368,6 +387,67 @@ class FineTuner:
         o, k = self.offsets[self.m.preprocess_model.p + "quantize.embedding.weight"]
         dist.broadcast(self.flat[o:o + k], src)
         dist.broadcast(self.embed_prob, src)
+
+
+class CapturedStep:
+    """The whole single-GPU fine-tune step (zero grads, forward, backward, AdamW) captured ONCE as a
+    hipGraph (torch.cuda.CUDAGraph) and replayed per step. At B=1 the eager step is host-bound
+    (~1,800 launches, each through torch autograd and ctypes); a replay issues them from the graph.
+    Inputs live in static buffers (copied in before each replay); AdamW's step-dependent scalars come
+    from a device buffer (rdeic_adamw_dev). Capture runs one eager warm-up step on a side stream
+    (packs the frozen layers' weights, sizes the workspaces) and then restores the optimizer state,
+    so the first replay is the tuner's next step. Multi-GPU steps stay eager (the bucketed all-reduce
+    is launched from the backward's hooks)."""
+
+    def __init__(self, ft: "FineTuner", img_u8: torch.Tensor, ctx: torch.Tensor, draws: dict):
+        if ft.buckets is not None:
+            raise ValueError("graph capture is single-GPU (the DDP all-reduce runs from backward hooks)")
+        self.ft = ft
+        self.img = img_u8.clone()
+        self.ctx = ctx.clone()
+        self.d = {k: (v.clone() if torch.is_tensor(v) else [x.clone() for x in v]) for k, v in draws.items()}
+        self.sc = torch.zeros(2, dtype=torch.float32, device=img_u8.device)
+        snap = [t.clone() for t in (ft.flat, ft.exp_avg, ft.exp_avg_sq, ft.embed_prob)]
+        step0 = ft.step_count
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ft.training_step(self.img, self.ctx, self.d)          # warm-up (eager)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=side):  # the stream the warm-up ran on
+            self.out = self._body()
+        for t, v in zip((ft.flat, ft.exp_avg, ft.exp_avg_sq, ft.embed_prob), snap):
+            t.copy_(v)
+        ft.step_count = step0
+        torch.cuda.synchronize()
+
+    def _body(self):
+        ft = self.ft
+        ft.zero_grad()
+        x_start, h = ft.get_first_stage(self.img, self.d["post_eps"])
+        with ops.splitk_allowed():
+            loss, d = ft.losses(x_start, h, self.ctx, self.d["t"], self.d["noise"], self.d["slice_noise"])
+            loss.backward()
+        d = {k: v.detach() for k, v in d.items()}
+        del loss
+        ft.adamw_launch(self.sc)
+        return d
+
+    def step(self, img_u8: torch.Tensor, draws: dict) -> dict:
+        ft = self.ft
+        self.img.copy_(img_u8, non_blocking=True)
+        for k, v in draws.items():
+            if torch.is_tensor(v):
+                self.d[k].copy_(v, non_blocking=True)
+            else:
+                for dst, src in zip(self.d[k], v):
+                    dst.copy_(src, non_blocking=True)
+        ft.step_count += 1
+        self.sc.copy_(ft.adam_scalars(ft.step_count), non_blocking=True)
+        self.graph.replay()
+        return self.out
 
 
 def nchw_draws_to_nhwc(dr: dict, device) -> dict:

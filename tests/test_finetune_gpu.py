@@ -242,3 +242,29 @@ def test_two_rank_ddp_step_equals_averaged_gradients(gpu):
     mask[o:o + k] = False
     diff = np.abs(ours[mask] - res[0][mask]).max()
     assert diff <= 1e-7, diff
+
+
+def test_captured_step_replays_the_eager_steps(gpu):
+    """CapturedStep (the whole step as one hipGraph) reproduces two eager steps bit for bit:
+    parameters, AdamW moments, VQ usage EMA and the loss dict."""
+    from rdeic_amd.finetune import CapturedStep, FineTuner, nchw_draws_to_nhwc
+    from rdeic_amd.rdeic import RDEIC
+    from rdeic_amd.synthetic import synth_context, synth_image, train_draws
+    ctx = synth_context().cuda()
+    imgs = [torch.from_numpy(synth_image(128, 128, 300 + i)).cuda()[None] for i in range(2)]
+    runs = []
+    for captured in (False, True):
+        m = RDEIC(compute_dtype=torch.float32).init_synthetic()
+        ft = FineTuner(m)
+        draws = [nchw_draws_to_nhwc(train_draws(1, 16, 16, m.cfg["compression"]["slice_ch"], 40 + i,
+                                                m.used_timesteps), "cuda") for i in range(2)]
+        cs = CapturedStep(ft, imgs[0], ctx, draws[0]) if captured else None
+        losses = []
+        for i in range(2):
+            d = cs.step(imgs[i], draws[i]) if captured else ft.training_step(imgs[i], ctx, draws[i])
+            losses.append({k: float(v.detach()) for k, v in d.items()})
+        torch.cuda.synchronize()
+        runs.append((ft.flat.cpu(), ft.exp_avg.cpu(), ft.exp_avg_sq.cpu(), ft.embed_prob.cpu(), losses))
+    (p0, m0, v0, e0, l0), (p1, m1, v1, e1, l1) = runs
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1) and torch.equal(e0, e1)
+    assert l0 == l1
