@@ -48,11 +48,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "finetune_ood.yaml"))
     ap.add_argument("--max-steps", type=int, default=None)
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step (one GPU)")
     args = ap.parse_args(argv)
     with open(args.config) as f:
         cfg = yaml.safe_load(f)
     from rdeic_amd import parallel
-    from rdeic_amd.finetune import FineTuneConfig, FineTuner, nchw_draws_to_nhwc
+    from rdeic_amd.finetune import CapturedStep, FineTuneConfig, FineTuner, nchw_draws_to_nhwc
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import synth_context, synth_image, train_draws
 
@@ -84,12 +85,16 @@ def main(argv=None):
     ck_dir = ck.get("dirpath", "./logs/ood_finetune")
     slice_ch = model.cfg["compression"]["slice_ch"]
     rng = np.random.default_rng(seed + rank)
+    graph = None
     t0 = time.perf_counter()
     for step in range(1, max_steps + 1):
         idx = rng.integers(0, n_img, size=B)
         dr = nchw_draws_to_nhwc(train_draws(B, S // 8, S // 8, slice_ch, seed * 1000003 + step * 131 + rank,
                                             ft.cfg.used_timesteps), dev)
-        d = ft.training_step(pool[torch.from_numpy(idx).to(dev)], ctx, dr)
+        batch = pool[torch.from_numpy(idx).to(dev)]
+        if world == 1 and not args.eager and graph is None:
+            graph = CapturedStep(ft, batch, ctx, dr)  # one GPU: the step replays as one hipGraph
+        d = graph.step(batch, dr) if graph is not None else ft.training_step(batch, ctx, dr)
         if rank == 0 and (step % log_every == 0 or step == max_steps):
             rec = {k: round(float(v), 6) for k, v in d.items()}
             rec.update(global_step=step, it_per_s=round(step / (time.perf_counter() - t0), 4))
