@@ -44,13 +44,55 @@ struct GemmArgs {
   float alpha, beta;
 };
 
-constexpr int GBM = 64, GBN = 64, GBK = 32;
+constexpr int GBK = 32;
 
-template <typename T>
+// Operand images in LDS. An operand whose k stride is 1 ("KC") is staged as rows of the tile's
+// m (or n) index with k contiguous, [TB][GBK + pad], and read as 8 consecutive k per lane. Any
+// other operand ("MN": m / n contiguous in memory, or generic strides) is staged as rows of k,
+// [GBK][TB], with one 16-byte write per 8 elements; bf16 lanes then read it with the gfx950
+// transposed read ds_read_b64_tr_b16 (two per 16x16x32 fragment, delivering the same k -> lane
+// mapping as the KC image, so both images give bit-identical products). The bf16 MN image has no
+// pad: its 32-byte slots are XOR-swizzled by the row (mn_swz) so that the eight rows one 32-lane
+// half reads (k = 8lg + q, lg = 0/1, q = 0..3) land on eight different bank groups. fp32 MN images
+// are read one element per lane (16x16x4 f32 operand) with a 16-float pad.
+template <int TB>
+__device__ __forceinline__ int mn_swz(int k) {
+  return TB == 128 ? ((k & 3) | (((k >> 3) & 1) << 2)) : (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+}
+template <typename T, int TB>
+__device__ __forceinline__ int mn_off(int k, int m) {  // element offset of (k, m) in an MN image
+  if constexpr (sizeof(T) == 2) return k * TB + ((((m >> 4) ^ mn_swz<TB>(k))) << 4) + (m & 15);
+  else return k * (TB + 16) + m;
+}
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+
+// the 8 k values (8lg .. 8lg+7) of row `r` of an MN bf16 image for this lane, as one MFMA operand
+template <int TB>
+__device__ __forceinline__ bf16x8 mn_frag(const bf16* S, int r0, int lane) {
+  const int lg = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int m = r0 + 4 * p;
+  const int k0 = 8 * lg + q;
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + mn_off<bf16, TB>(k0, m)));
+  const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(S + mn_off<bf16, TB>(k0 + 4, m)));
+  // one shuffle + bit cast (element-wise __bf16 inserts were packed wrongly by this compiler)
+  typedef short short8v __attribute__((ext_vector_type(8)));
+  const short8v r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// TB x TB tile (64 or 128), 4 waves of (TB/2)^2; each thread stages TB/64 groups of 8 elements per
+// operand. AKC / BKC: the operand's k stride is 1 (KC image), else MN image (see above).
+template <typename T, int TB, bool AKC, bool BKC>
 __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
   constexpr int PAD = sizeof(T) == 2 ? 8 : 4;
-  __shared__ __attribute__((aligned(16))) T As[GBM][GBK + PAD];
-  __shared__ __attribute__((aligned(16))) T Bs[GBN][GBK + PAD];
+  constexpr int G = TB / 64, TF = TB / 32;  // staging groups per thread, 16x16 fragments per wave dim
+  constexpr int KC_ELEMS = TB * (GBK + PAD);
+  constexpr int MN_ELEMS = sizeof(T) == 2 ? GBK * TB : GBK * (TB + 16);
+  constexpr int A_ELEMS = AKC ? KC_ELEMS : MN_ELEMS, B_ELEMS = BKC ? KC_ELEMS : MN_ELEMS;
+  __shared__ __attribute__((aligned(16))) T As[A_ELEMS];
+  __shared__ __attribute__((aligned(16))) T Bs[B_ELEMS];
   const int z = blockIdx.z, z1 = z / g.nb2, z2 = z - z1 * g.nb2;
   const T* A = (const T*)g.a + z2 * g.a_bs2;
   const T* B = (const T*)g.b + z2 * g.b_bs2;
@@ -64,17 +106,16 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
     A += z1 * g.a_bs1;
     B += z1 * g.b_bs1;
   }
-  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+  const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-  const bool a_kc = g.a_sk == 1, b_kc = g.b_sk == 1;
-  // per-thread staging coordinates (8 elements of A and of B per k-tile)
-  const int ar = a_kc ? (tid >> 2) : ((tid & 7) * 8), ak = a_kc ? ((tid & 3) * 8) : (tid >> 3);
-  const int br = b_kc ? (tid >> 2) : ((tid & 7) * 8), bk = b_kc ? ((tid & 3) * 8) : (tid >> 3);
-  T ra[8], rb[8];
-  // 8 elements a thread stages per operand are contiguous in memory when the staged dimension has
-  // stride 1 (k for a_kc / b_kc, else m / n): one (bf16) or two (fp32) 16-byte loads when aligned and
-  // in bounds, element loads otherwise
-  const bool a_vec = a_kc || g.a_sm == 1, b_vec = b_kc || g.b_sn == 1;
+  // staging coordinates of group 0 (group q adds 64 rows of m / n)
+  const int ar = AKC ? (tid >> 2) : ((tid & 7) * 8), ak = AKC ? ((tid & 3) * 8) : (tid >> 3);
+  const int br = BKC ? (tid >> 2) : ((tid & 7) * 8), bk = BKC ? ((tid & 3) * 8) : (tid >> 3);
+  T ra[G][8], rb[G][8];
+  // the 8 elements of a group are contiguous in memory when the staged dimension has stride 1
+  // (k for KC, else m / n): one (bf16) or two (fp32) 16-byte loads when aligned and in bounds,
+  // element loads otherwise
+  const bool a_vec = AKC || g.a_sm == 1, b_vec = BKC || g.b_sn == 1;
   auto load8 = [&](const T* base, long step, bool contiguous, int valid, T (&r)[8]) {
     if (contiguous && valid == 8 && ((uintptr_t)base & 15) == 0) {
       if constexpr (sizeof(T) == 2) {
@@ -89,82 +130,87 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
     }
   };
   auto load = [&](long k0) {
-    if (a_kc) {
-      const long kk = k0 + ak;
-      const int valid = (m0 + ar < g.m) ? (int)max(0L, min(8L, klen - kk)) : 0;
-      load8(A + (long)(m0 + ar) * g.a_sm + kk, 1, true, valid, ra);
-    } else {
-      const long kk = k0 + ak;
-      const int valid = kk < klen ? max(0, min(8, g.m - (m0 + ar))) : 0;
-      load8(A + (long)(m0 + ar) * g.a_sm + kk * g.a_sk, g.a_sm, a_vec, valid, ra);
-    }
-    if (b_kc) {
-      const long kb = k0 + bk;
-      const int valid = (n0 + br < g.n) ? (int)max(0L, min(8L, klen - kb)) : 0;
-      load8(B + kb + (long)(n0 + br) * g.b_sn, 1, true, valid, rb);
-    } else {
-      const long kb = k0 + bk;
-      const int valid = kb < klen ? max(0, min(8, g.n - (n0 + br))) : 0;
-      load8(B + kb * g.b_sk + (long)(n0 + br) * g.b_sn, g.b_sn, b_vec, valid, rb);
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int arq = ar + 64 * q, brq = br + 64 * q;
+      const long kk = k0 + ak, kb = k0 + bk;
+      if constexpr (AKC) {
+        const int valid = (m0 + arq < g.m) ? (int)max(0L, min(8L, klen - kk)) : 0;
+        load8(A + (long)(m0 + arq) * g.a_sm + kk, 1, true, valid, ra[q]);
+      } else {
+        const int valid = kk < klen ? max(0, min(8, g.m - (m0 + arq))) : 0;
+        load8(A + (long)(m0 + arq) * g.a_sm + kk * g.a_sk, g.a_sm, a_vec, valid, ra[q]);
+      }
+      if constexpr (BKC) {
+        const int valid = (n0 + brq < g.n) ? (int)max(0L, min(8L, klen - kb)) : 0;
+        load8(B + kb + (long)(n0 + brq) * g.b_sn, 1, true, valid, rb[q]);
+      } else {
+        const int valid = kb < klen ? max(0, min(8, g.n - (n0 + brq))) : 0;
+        load8(B + kb * g.b_sk + (long)(n0 + brq) * g.b_sn, g.b_sn, b_vec, valid, rb[q]);
+      }
     }
   };
-  f32x4 acc[2][2];
+  auto store16 = [&](T* dst, const T (&r)[8]) {
+    if constexpr (sizeof(T) == 2) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(r);
+    else { reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(r)[0];
+           reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(r)[1]; }
+  };
+  auto store = [&](T* S, bool kc, int r0, int k0s, const T (&r)[8]) {
+    if (kc) store16(S + r0 * (GBK + PAD) + k0s, r);
+    else store16(S + mn_off<T, TB>(k0s, r0), r);
+  };
+  f32x4 acc[TF][TF];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TF; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wm = (wave >> 1) * (TB / 2), wn = (wave & 1) * (TB / 2);
   load(0);
   for (long k0 = 0; k0 < klen; k0 += GBK) {
     __syncthreads();
-    if (a_kc) {
-      if constexpr (sizeof(T) == 2) *reinterpret_cast<uint4*>(&As[ar][ak]) = *reinterpret_cast<const uint4*>(ra);
-      else { reinterpret_cast<uint4*>(&As[ar][ak])[0] = reinterpret_cast<const uint4*>(ra)[0];
-             reinterpret_cast<uint4*>(&As[ar][ak])[1] = reinterpret_cast<const uint4*>(ra)[1]; }
-    } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) As[ar + e][ak] = ra[e];
-    }
-    if (b_kc) {
-      if constexpr (sizeof(T) == 2) *reinterpret_cast<uint4*>(&Bs[br][bk]) = *reinterpret_cast<const uint4*>(rb);
-      else { reinterpret_cast<uint4*>(&Bs[br][bk])[0] = reinterpret_cast<const uint4*>(rb)[0];
-             reinterpret_cast<uint4*>(&Bs[br][bk])[1] = reinterpret_cast<const uint4*>(rb)[1]; }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Bs[br + e][bk] = rb[e];
+    for (int q = 0; q < G; ++q) {
+      store(As, AKC, ar + 64 * q, ak, ra[q]);
+      store(Bs, BKC, br + 64 * q, bk, rb[q]);
     }
     __syncthreads();
     if (k0 + GBK < klen) load(k0 + GBK);
     if constexpr (sizeof(T) == 2) {
-      bf16x8 af[2], bfr[2];
+      bf16x8 af[TF], bfr[TF];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(&As[wm + 16 * i + lr][8 * lg]);
+      for (int i = 0; i < TF; ++i)
+        af[i] = AKC ? *reinterpret_cast<const bf16x8*>(&As[(wm + 16 * i + lr) * (GBK + PAD) + 8 * lg])
+                    : mn_frag<TB>(As, wm + 16 * i, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[wn + 16 * j + lr][8 * lg]);
+      for (int j = 0; j < TF; ++j)
+        bfr[j] = BKC ? *reinterpret_cast<const bf16x8*>(&Bs[(wn + 16 * j + lr) * (GBK + PAD) + 8 * lg])
+                     : mn_frag<TB>(Bs, wn + 16 * j, lane);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TF; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     } else {
 #pragma unroll
       for (int s = 0; s < GBK / 4; ++s) {
-        float af[2], bfr[2];
+        float af[TF], bfr[TF];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = As[wm + 16 * i + lr][4 * s + lg];
+        for (int i = 0; i < TF; ++i)
+          af[i] = AKC ? As[(wm + 16 * i + lr) * (GBK + PAD) + 4 * s + lg] : As[mn_off<T, TB>(4 * s + lg, wm + 16 * i + lr)];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bfr[j] = Bs[wn + 16 * j + lr][4 * s + lg];
+        for (int j = 0; j < TF; ++j)
+          bfr[j] = BKC ? Bs[(wn + 16 * j + lr) * (GBK + PAD) + 4 * s + lg] : Bs[mn_off<T, TB>(4 * s + lg, wn + 16 * j + lr)];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TF; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
   }
   const long coff = z1 * g.c_bs1 + z2 * g.c_bs2;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TF; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TF; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int mm = m0 + wm + 16 * i + 4 * lg + r, nn = n0 + wn + 16 * j + lr;
@@ -181,6 +227,15 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
           cp[ci] = from_f32<T>(v);
         }
       }
+}
+
+template <typename T, int TB>
+void launch_gemm(const GemmArgs& g, dim3 grid, hipStream_t s) {
+  const bool akc = g.a_sk == 1, bkc = g.b_sk == 1;
+  if (akc && bkc) hipLaunchKernelGGL((gemm_strided_kernel<T, TB, true, true>), grid, dim3(256), 0, s, g);
+  else if (akc) hipLaunchKernelGGL((gemm_strided_kernel<T, TB, true, false>), grid, dim3(256), 0, s, g);
+  else if (bkc) hipLaunchKernelGGL((gemm_strided_kernel<T, TB, false, true>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_strided_kernel<T, TB, false, false>), grid, dim3(256), 0, s, g);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -985,15 +1040,21 @@ extern "C" int rdeic_gemm_strided(const rdeic_gemm_desc* d, void* stream) {
   g.c = d->c; g.c_bs1 = d->c_bs1; g.c_bs2 = d->c_bs2; g.c_sm = d->c_sm;
   g.nb2 = d->nb2; g.m = d->m; g.n = d->n; g.k = d->k; g.ksplit = d->ksplit; g.c_f32 = d->c_f32;
   g.alpha = d->alpha; g.beta = d->beta;
-  dim3 grid((d->n + GBN - 1) / GBN, (d->m + GBM - 1) / GBM, d->batch);
   if (d->batch > 65535) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const double flops = 2.0 * d->m * d->n * (d->ksplit > 0 ? (double)d->k : (double)d->k * (d->batch / d->nb2)) * d->nb2;
   ProfScope ps(s, RDEIC_PROF_GEMM, flops);
-  if (d->dtype == 1)
-    hipLaunchKernelGGL(gemm_strided_kernel<bf16>, grid, dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL(gemm_strided_kernel<float>, grid, dim3(256), 0, s, g);
+  // 128x128 tiles where their grid still has ~a workgroup per CU, else 64x64
+  const long t128 = (long)((d->n + 127) / 128) * ((d->m + 127) / 128) * d->batch;
+  if (d->m >= 128 && d->n >= 128 && t128 >= 200) {
+    dim3 grid((d->n + 127) / 128, (d->m + 127) / 128, d->batch);
+    if (d->dtype == 1) launch_gemm<bf16, 128>(g, grid, s);
+    else launch_gemm<float, 128>(g, grid, s);
+  } else {
+    dim3 grid((d->n + 63) / 64, (d->m + 63) / 64, d->batch);
+    if (d->dtype == 1) launch_gemm<bf16, 64>(g, grid, s);
+    else launch_gemm<float, 64>(g, grid, s);
+  }
   return launch_status();
 }
 

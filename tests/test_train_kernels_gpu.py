@@ -25,10 +25,12 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("layout", ["nn", "tn", "nt", "tt"])
-def test_gemm_strided(gpu, dt, layout):
+@pytest.mark.parametrize("shape", [(70, 130, 100, 3, 4), (260, 390, 200, 20, 32)],
+                         ids=["tile64", "tile128"])  # (m, n, k, batch, split-K planes); ragged edges
+def test_gemm_strided(gpu, dt, layout, shape):
     from rdeic_amd import autograd as AG
     g = torch.Generator(device="cuda").manual_seed(1)
-    m, n, k, nb = 70, 130, 100, 3
+    m, n, k, nb, planes = shape
     A = torch.randn((nb, m, k), device="cuda", generator=g)
     B = torch.randn((nb, k, n), device="cuda", generator=g)
     ref = torch.bmm(A.to(dt).float(), B.to(dt).float())
@@ -43,9 +45,10 @@ def test_gemm_strided(gpu, dt, layout):
     tol = 1e-5 if dt == torch.float32 else 1e-2
     assert _rel(C, ref) < tol
     # split-K planes sum to the product
-    P = torch.empty((4, m, n), device="cuda", dtype=torch.float32)
-    AG.gemm(a_st[0], 0, a_sm, a_sk, b_st[0], 0, b_sk, b_sn, P, 0, n, m=m, n=n, k=k, batch=4, c_bs=(m * n, 0),
-            ksplit=32)
+    ks = -(-k // planes)
+    P = torch.empty((planes, m, n), device="cuda", dtype=torch.float32)
+    AG.gemm(a_st[0], 0, a_sm, a_sk, b_st[0], 0, b_sk, b_sn, P, 0, n, m=m, n=n, k=k, batch=planes, c_bs=(m * n, 0),
+            ksplit=ks)
     assert _rel(P.sum(0), ref[0]) < tol
 
 
