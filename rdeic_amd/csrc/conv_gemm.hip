@@ -1254,6 +1254,10 @@ static int conv2d_run(const rdeic_conv_desc* d, void* stream, bool* fused) {
     return launch_cfg<bf16, 128, 128, 2, 2>(a, vec, s);
   } else {
     if (d->cout <= 16) return launch_cfg<float, 64, 16, 4, 1>(a, vec, s);
+    // 128x128 tiles (64x64 per wave: 4096 MFMA cycles per k-tile hide the single-stage prefetch)
+    // where their grid still fills the chip; same k order as 64x64, so bit-identical
+    if (d->cout >= 128 && (long)cdiv(a.M, 128) * cdiv(a.cout, 128) * a.batch >= 512)
+      return launch_cfg<float, 128, 128, 2, 2>(a, vec, s);
     return launch_cfg<float, 64, 64, 2, 2>(a, vec, s);
   }
 }
@@ -1307,7 +1311,7 @@ static int conv2d_impl(const rdeic_conv_desc* d, int32_t tile, void* stream) {
 
 // Split-K variant (small-M, large-K layers): `splits` k-ranges computed into a caller-provided
 // fp32 workspace of splits * M * cout floats, then reduced in split order (deterministic) with
-// the bias / emb / activation / residual epilogue. bf16, 16-byte gathers, no GN prologue,
+// the bias / emb / activation / residual epilogue. bf16 or fp32, 16-byte gathers, no GN prologue,
 // out_mode 0, batch 1, cout % 8 == 0. The k-order differs from rdeic_conv2d (not bit-identical
 // to it), so callers that need batch invariance must not use it.
 static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats,
@@ -1316,11 +1320,27 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
   bool vec = false;
   const int rc = make_args(d, a, vec);
   if (rc != RDEIC_OK) return rc;
-  if (d->dtype != 1 || !vec || d->gn_ab || d->out_mode != 0 || a.batch != 1 || d->cout % 8 || splits < 2 || !ws ||
+  if (!vec || d->gn_ab || d->out_mode != 0 || a.batch != 1 || d->cout % 8 || splits < 2 || !ws ||
       (d->out_ld % 8) || ((uintptr_t)d->out % 16) || ((uintptr_t)ws % 16))
     return RDEIC_EINVAL;
   if (ws_floats < (size_t)splits * a.M * a.cout) return RDEIC_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
+  if (d->dtype == 0) {  // fp32: 64x64 register-staged partial tiles, fp32 output from the reduction
+    ConvArgs p = a;
+    p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr;
+    p.out = (char*)ws; p.out_ld = a.cout; p.out_f32 = 0;
+    p.splits = splits;
+    p.kper = (a.nk + splits - 1) / splits;
+    dim3 grid(cdiv(a.M, 64), cdiv(a.cout, 64), splits);
+    constexpr int lds = conv_lds_bytes<float, 64, 64>();
+    hipLaunchKernelGGL((conv_kernel<float, 64, 64, 2, 2, true, false, false, true>), grid, dim3(256), lds, s, p);
+    a.splits = splits;
+    a.out_f32 = 1;  // the reduction's output (and residual) type: fp32
+    const long chunks = (long)a.M * (a.cout / 8);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, a,
+                       (const float*)ws);
+    return launch_status();
+  }
   if (g_dma && dma_grouped(d, -1, splits, ws, s) == RDEIC_OK) {
     a.splits = splits;
     const long chunks = (long)a.M * (a.cout / 8);

@@ -304,11 +304,18 @@ class splitk_allowed:
 
 def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor) -> int:
     """Number of k-splits (1 = none): only when the 128x128 tile grid cannot fill the chip."""
-    if not SPLITK_ALLOWED or fused or x.dtype != torch.bfloat16 or p.cout % 8 or pix_ld(out) % 8:
+    if not SPLITK_ALLOWED or fused or x.dtype not in (torch.bfloat16, torch.float32) or p.cout % 8 \
+            or pix_ld(out) % 8 or out.data_ptr() % 16:
         return 1
     for t in (x, x2):
         if t is not None and (t.shape[3] % 8 or pix_ld(t) % 8 or t.data_ptr() % 16):
             return 1
+    if x.dtype == torch.float32:  # 64x64 fp32 tiles, 32-deep k-steps
+        tiles = -(-M // 64) * -(-p.cout // 64)
+        nk = -(-(p.kh * p.kw * p.cin) // 32)
+        if tiles >= 256 or nk < 32:
+            return 1
+        return max(1, min(-(-512 // tiles), nk // 8, 16))
     tiles = -(-M // 128) * -(-p.cout // 128)
     nk = -(-(p.kh * p.kw * p.cin) // 64)
     if tiles >= 192 or nk < 32:

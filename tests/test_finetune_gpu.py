@@ -190,7 +190,7 @@ def test_two_rank_ddp_step_equals_averaged_gradients(gpu):
     applying AdamW to the mean of the two single-image gradients."""
     import socket
     import torch.multiprocessing as mp
-    from rdeic_amd import autograd as AG
+    from rdeic_amd import autograd as AG, ops
     from rdeic_amd.finetune import FineTuner, nchw_draws_to_nhwc
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import synth_context, synth_image, train_draws
@@ -225,8 +225,9 @@ def test_two_rank_ddp_step_equals_averaged_gradients(gpu):
         d = nchw_draws_to_nhwc(dr, "cuda")
         img = torch.from_numpy(synth_image(128, 128, 231 + r)).cuda()[None]
         x_start, h = ft.get_first_stage(img, d["post_eps"])
-        loss, _ = ft.losses(x_start, h, synth_context().cuda(), d["t"], d["noise"], d["slice_noise"])
-        loss.backward()
+        with ops.splitk_allowed():  # as FineTuner.training_step runs it
+            loss, _ = ft.losses(x_start, h, synth_context().cuda(), d["t"], d["noise"], d["slice_noise"])
+            loss.backward()
         gsum += ft.grad
         if r == 0:
             E_fwd0 = ft.p("preprocess_model.quantize.embedding.weight").detach().clone()

@@ -43,6 +43,24 @@ def test_conv2d(gpu, dtype, cin, cout, k, stride, pad, h):
     torch.testing.assert_close(_nchw(out), ref, rtol=rt, atol=at * ref.abs().max().item())
 
 
+def test_conv2d_fp32_large_tile(gpu):
+    """fp32 layers with >= 512 128x128 tiles (the VAE encoder at 512^2 in the fine-tune step) run
+    the 128x128 tile: vs torch fp32, with GN/SiLU prologue and residual."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(1, 128, 256, 256, generator=g)
+    w = torch.randn(128, 128, 3, 3, generator=g) / math.sqrt(128 * 9)
+    b = torch.randn(128, generator=g)
+    r = torch.randn(1, 128, 256, 256, generator=g)
+    gamma, beta = torch.rand(128, generator=g) + 0.5, torch.randn(128, generator=g) * 0.1
+    ref = F.conv2d(F.silu(F.group_norm(x, 32, gamma, beta, eps=1e-6)), w, b, padding=1) + r
+    p = ops.ConvParams.pack(w, b, pad=1, dtype=torch.float32)
+    xd = _nhwc(x)
+    ab = ops.group_norm_ab(xd, gamma.cuda(), beta.cuda(), 32, 1e-6)
+    out = ops.conv2d(xd, p, gn=ab, gn_silu=True, res=_nhwc(r))
+    torch.testing.assert_close(_nchw(out), ref, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv2d_fusions(gpu, dtype):
     """concat + GN/SiLU prologue + emb + leaky + residual; up2; asymmetric pad; pixel shuffle."""
@@ -263,6 +281,32 @@ def test_conv_splitk(gpu, cin, cout, hw, res):
     torch.testing.assert_close(_nchw(out), ref, rtol=2e-2, atol=3e-2)
     out_plain = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
     assert (out.float() - out_plain.float()).abs().max().item() < 0.1
+
+
+@pytest.mark.parametrize("cin,cout,hw,k,res", [(1280, 1280, 8, 3, True), (256, 256, 16, 3, False),
+                                               (1280, 1280, 16, 1, True)])
+def test_conv_splitk_fp32(gpu, cin, cout, hw, k, res):
+    """fp32 split-K conv (the fine-tune step's B=1 small-M layers) vs torch fp32, and vs the
+    unsplit fp32 kernel."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(cin + hw + k)
+    x = torch.randn(1, cin, hw, hw, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / math.sqrt(cin * k * k)
+    b = torch.randn(cout, generator=g)
+    emb = torch.randn(1, cout, generator=g)
+    r = torch.randn(1, cout, hw, hw, generator=g)
+    ref = F.silu(F.conv2d(x, w, b, padding=k // 2) + emb[:, :, None, None])
+    if res:
+        ref = ref + r
+    p = ops.ConvParams.pack(w, b, pad=k // 2, dtype=torch.float32)
+    xd, rd = _nhwc(x), _nhwc(r)
+    with ops.splitk_allowed():
+        assert ops._splitk_count(xd, None, hw * hw, p, False, rd) > 1
+        out = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
+    assert out.dtype == torch.float32
+    torch.testing.assert_close(_nchw(out), ref, rtol=1e-4, atol=1e-4)
+    out_plain = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
+    torch.testing.assert_close(out, out_plain, rtol=1e-4, atol=5e-5)
 
 
 @pytest.mark.parametrize("rows,cin,inner", [(4096, 320, 1280), (1000, 640, 2560), (256, 64, 256)])
