@@ -165,7 +165,38 @@ def conv_dgrad(dz: torch.Tensor, weight: torch.Tensor, cfg: ConvCfg, in_hw, froz
     return d_in
 
 
-def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, cfg: ConvCfg, cout: int, cin: int, out=None) -> torch.Tensor:
+# Direct gradients: a trainable parameter may carry `_rdeic_gview` (its fp32 gradient view, e.g. a
+# slice of FineTuner's flat buffer) and `_rdeic_notify` (called once its gradient is complete, e.g.
+# the DDP bucket counter). The conv / linear backward then accumulates the weight and bias gradients
+# straight into the view (the finalize kernels' accumulate mode) and returns None for them, so
+# autograd runs no AccumulateGrad add per parameter. The sums equal AccumulateGrad's (0 + g = g).
+# A parameter used by several layers (the checkerboard entropy nets run on the anchor and the
+# non-anchor half) is notified after its last use's gradient: the forward counts the uses that
+# will run a backward, each backward contribution counts one down.
+def direct_grad_view(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    return None if t is None else getattr(t, "_rdeic_gview", None)
+
+
+def count_direct_use(t: Optional[torch.Tensor], needs_grad: bool) -> Optional[torch.Tensor]:
+    """Forward side (needs_grad: the Function's ctx.needs_input_grad entry for t — grad mode itself
+    is off inside Function.forward): the parameter if its gradient will go to its direct view."""
+    if direct_grad_view(t) is None or not needs_grad:
+        return None
+    t._rdeic_uses = getattr(t, "_rdeic_uses", 0) + 1
+    t._rdeic_direct = True  # autograd still runs the leaf's AccumulateGrad (on no gradient): hooks skip it
+    return t
+
+
+def notify_grad(t: torch.Tensor) -> None:
+    t._rdeic_uses -= 1
+    if t._rdeic_uses == 0:
+        fn = getattr(t, "_rdeic_notify", None)
+        if fn is not None:
+            fn(t)
+
+
+def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, cfg: ConvCfg, cout: int, cin: int, out=None,
+               accumulate: bool = False) -> torch.Tensor:
     """fp32 [cout, cin, kh, kw] = dz^T . im2col(x) (split-K over pixels, fixed-order reduction)."""
     n, ho, wo, _ = dz.shape
     P = n * ho * wo
@@ -187,7 +218,8 @@ def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, cfg: ConvCfg, cout: int, cin: 
     gemm(dz, 0, 1, ldz, cols, 0, b_sk, 1, part, 0, K, m=cout, n=K, k=P, batch=splits, c_bs=(cout * K, 0), ksplit=ks)
     if out is None:
         out = torch.empty((cout, cin, cfg.kh, cfg.kw), dtype=torch.float32, device=x.device)
-    call("rdeic_wgrad_finalize", part.data_ptr(), splits, cout, cin, cfg.kh, cfg.kw, out.data_ptr(), 0, _sp())
+    call("rdeic_wgrad_finalize", part.data_ptr(), splits, cout, cin, cfg.kh, cfg.kw, out.data_ptr(), int(accumulate),
+         _sp())
     return out
 
 
@@ -213,8 +245,9 @@ def _conv_forward(x, weight, bias, emb, res, cfg: ConvCfg):
     return out, z
 
 
-def _conv_backward(x, weight, z, dout, cfg: ConvCfg, in_hw, need_x, need_w, need_b, need_emb):
-    """(dx, dw, db, demb) of _conv_forward given the output gradient (dres = dout)."""
+def _conv_backward(x, weight, z, dout, cfg: ConvCfg, in_hw, need_x, need_w, need_b, need_emb, bias=None):
+    """(dx, dw, db, demb) of _conv_forward given the output gradient (dres = dout). dw / db are None
+    when they went straight into the parameters' direct gradient views (direct_grad_view)."""
     dz = dout
     if cfg.act != NONE:
         rows, c, ldz = _rows_view(z)
@@ -237,9 +270,19 @@ def _conv_backward(x, weight, z, dout, cfg: ConvCfg, in_hw, need_x, need_w, need
     if need_x:
         dx = conv_dgrad(dz, weight, cfg, in_hw, frozen=not weight.requires_grad)
     if need_w:
-        dw = conv_wgrad(x, dz, cfg, cout, cin).view(weight.shape)
+        gv = direct_grad_view(weight) if getattr(weight, "_rdeic_uses", 0) > 0 else None
+        if gv is not None:
+            conv_wgrad(x, dz, cfg, cout, cin, out=gv, accumulate=True)
+            notify_grad(weight)
+        else:
+            dw = conv_wgrad(x, dz, cfg, cout, cin).view(weight.shape)
     if need_b:
-        db = col_sum(dz, n * ho * wo, cout, cout).view(cout)
+        gv = direct_grad_view(bias)  # bias is passed only when counted in the forward
+        if gv is not None:
+            col_sum(dz, n * ho * wo, cout, cout, out=gv.view(1, cout), accumulate=True)
+            notify_grad(bias)
+        else:
+            db = col_sum(dz, n * ho * wo, cout, cout).view(cout)
     if need_emb:
         demb = col_sum(dz, n * ho * wo, cout, cout, groups=n)
     return dx, dw, db, demb
@@ -254,6 +297,8 @@ class Conv2dFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.flags = (emb is not None, res is not None, bias is not None)
         ctx.in_hw = (x.shape[1], x.shape[2])
+        count_direct_use(weight, ctx.needs_input_grad[1])
+        ctx.bias = count_direct_use(bias, ctx.needs_input_grad[2])  # a leaf parameter
         ctx.save_for_backward(x, weight, z)
         return out
 
@@ -264,7 +309,7 @@ class Conv2dFn(torch.autograd.Function):
         dout = dout.contiguous()
         nig = ctx.needs_input_grad
         dx, dw, db, demb = _conv_backward(x, weight, z, dout, ctx.cfg, ctx.in_hw, nig[0], nig[1],
-                                          has_bias and nig[2], has_emb and nig[3])
+                                          has_bias and nig[2], has_emb and nig[3], bias=ctx.bias)
         return dx, dw, db, demb, (dout if has_res else None), None
 
 
@@ -287,6 +332,8 @@ class LinearFn(torch.autograd.Function):
         out, _ = _conv_forward(_tok4(x), weight, bias, None, None if res is None else _tok4(res), cfg)
         ctx.cfg = cfg
         ctx.flags = (res is not None, bias is not None)
+        count_direct_use(weight, ctx.needs_input_grad[1])
+        ctx.bias = count_direct_use(bias, ctx.needs_input_grad[2])
         ctx.save_for_backward(x, weight)
         return out.view(rows, weight.shape[0])
 
@@ -298,7 +345,7 @@ class LinearFn(torch.autograd.Function):
         rows = x.shape[0]
         nig = ctx.needs_input_grad
         dx, dw, db, _ = _conv_backward(_tok4(x), weight, None, _tok4(dout), ctx.cfg, (rows, 1), nig[0], nig[1],
-                                       has_bias and nig[2], False)
+                                       has_bias and nig[2], False, bias=ctx.bias)
         if dx is not None:
             dx = dx.view(rows, weight.shape[1])
         return dx, dw, db, (dout if has_res else None), None

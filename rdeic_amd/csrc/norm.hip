@@ -54,10 +54,18 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x
     const int ch0 = t % cs, pl = t / cs;
     const float K = to_f32(xi[ch0]);
     float s1 = 0.f, s2 = 0.f;
-    for (int p = p0 + pl; p < p1; p += PL) {
-      float v = to_f32(xi[(long)p * ld + ch0]) - K;
-      s1 += v;
-      s2 += v * v;
+    // 16 loads in flight per thread, then the pixel-ordered sums (same order as one at a time)
+    for (int p = p0 + pl; p < p1; p += 16 * PL) {
+      float y[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) y[u] = p + u * PL < p1 ? to_f32(xi[(long)(p + u * PL) * ld + ch0]) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if (p + u * PL >= p1) break;
+        float v = y[u] - K;
+        s1 += v;
+        s2 += v * v;
+      }
     }
     red[0][t] = s1;
     red[1][t] = s2;
@@ -72,10 +80,17 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x
     for (int ch0 = t; ch0 < cs; ch0 += 256) {
       const float K = to_f32(xi[ch0]);
       float s1 = 0.f, s2 = 0.f;
-      for (int p = p0; p < p1; ++p) {
-        float v = to_f32(xi[(long)p * ld + ch0]) - K;
-        s1 += v;
-        s2 += v * v;
+      for (int p = p0; p < p1; p += 16) {
+        float y[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) y[u] = p + u < p1 ? to_f32(xi[(long)(p + u) * ld + ch0]) : 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          if (p + u >= p1) break;
+          float v = y[u] - K;
+          s1 += v;
+          s2 += v * v;
+        }
       }
       float* o = part + (((long)img * nchunk + chunk) * c + coff + ch0) * 2;
       o[0] = s1;

@@ -71,6 +71,7 @@ class FineTuner:
             p = self.flat[off:off + k].view(shape)
             p.requires_grad_(True)
             p.grad = self.grad[off:off + k].view(shape)
+            p._rdeic_gview = p.grad  # conv / linear backward accumulate here directly (autograd.direct_grad_view)
             st.t[n] = p
             self.offsets[n] = (off, k)
             off += k
@@ -333,6 +334,10 @@ class FineTuner:
 
     def zero_grad(self):
         self.grad.zero_()
+        for n in self.offsets:  # direct-gradient use counts (autograd.count_direct_use) start at zero
+            p = self.m.store.t[n]
+            p._rdeic_uses = 0
+            p._rdeic_direct = False
 
     def adam_scalars(self, step: int) -> torch.Tensor:
         """[-lr / (1 - beta1^step), sqrt(1 - beta2^step)] in Python doubles, as torch.optim.AdamW forms them."""

@@ -115,7 +115,12 @@ class GradBuckets:
         if cur_hi is not None:
             self.buckets.append((cur_lo, cur_hi))
             self.count.append(members)
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p, _, _ in params]
+        # gradients arrive through AccumulateGrad (post-accumulate hook) or, for parameters with a
+        # direct gradient view (autograd.direct_grad_view), from the backward kernels' caller
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_hook) for p, _, _ in params]
+        self._params = [p for p, _, _ in params]
+        for p in self._params:
+            p._rdeic_notify = self._on_grad
         self.pending, self.handles, self.fired = [], {}, {}
 
     def begin(self):
@@ -129,6 +134,10 @@ class GradBuckets:
             self.handles[b] = dist.all_reduce(self.grad[lo:hi], group=self.group, async_op=True)
         else:
             self.handles[b] = None
+
+    def _on_hook(self, p):
+        if not getattr(p, "_rdeic_direct", False):  # direct-gradient parameters report through _on_grad
+            self._on_grad(p)
 
     def _on_grad(self, p):
         k = id(p)
@@ -155,3 +164,7 @@ class GradBuckets:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for p in self._params:
+            if getattr(p, "_rdeic_notify", None) == self._on_grad:
+                p._rdeic_notify = None
+        self._params = []

@@ -9,7 +9,7 @@ rc=$?
 tail -3 $O/pytest.log
 if [ $rc -gt 1 ]; then echo "stop: tests rc=$rc"; exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o train -- python3 $R/bench_train.py --steps 2 --warmup 1 --dtype bf16 --no-roofline > $O/bt.json 2> $O/bt.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o train -- python3 $R/bench_train.py --steps 2 --warmup 1 --dtype ${TRACE_DTYPE:-bf16} --no-roofline > $O/bt.json 2> $O/bt.err
 rc=$?
 echo "rocprof rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
