@@ -351,16 +351,30 @@ __global__ void wgrad_finalize_kernel(const float* __restrict__ part, int splits
 }
 
 // column sums: stage 1 per (group, row chunk), stage 2 over chunks in order
-constexpr int CS_ROWS = 32;  // rows per stage-1 block (B=1 training shapes: enough blocks to fill the chip)
+// Rows per stage-1 block: 32 (B=1 training shapes: enough blocks to fill the chip), growing with
+// the row count so that stage 2 sums at most 256 partials per column.
+inline long cs_rows(long rows_per_group) {
+  long r = 32;
+  while ((rows_per_group + r - 1) / r > 256) r *= 2;
+  return r;
+}
 template <typename T>
 __global__ void col_sum_partial_kernel(const T* __restrict__ x, long rows_per_group, int c, int ld, int nchunk,
-                                       float* __restrict__ ws) {
+                                       long rpc, float* __restrict__ ws) {
   const int grp = blockIdx.z, chunk = blockIdx.y, ch = blockIdx.x * 256 + threadIdx.x;
   if (ch >= c) return;
-  const long r0 = (long)chunk * CS_ROWS, r1 = min(rows_per_group, r0 + CS_ROWS);
+  const long r0 = (long)chunk * rpc, r1 = min(rows_per_group, r0 + rpc);
   const T* xp = x + ((long)grp * rows_per_group) * ld + ch;
   float s = 0.f;
-  for (long r = r0; r < r1; ++r) s += to_f32(xp[r * ld]);
+  long r = r0;
+  for (; r + 8 <= r1; r += 8) {  // 8 loads in flight, then the row-ordered adds
+    float y[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) y[u] = to_f32(xp[(r + u) * ld]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += y[u];
+  }
+  for (; r < r1; ++r) s += to_f32(xp[r * ld]);
   ws[((long)grp * nchunk + chunk) * c + ch] = s;
 }
 
@@ -369,8 +383,17 @@ __global__ void col_sum_final_kernel(const float* __restrict__ ws, int groups, i
   const long total = (long)groups * c;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int grp = (int)(i / c), ch = (int)(i - (long)grp * c);
+    const float* w = ws + (long)grp * nchunk * c + ch;
     float s = 0.f;
-    for (int q = 0; q < nchunk; ++q) s += ws[((long)grp * nchunk + q) * c + ch];
+    int q = 0;
+    for (; q + 8 <= nchunk; q += 8) {
+      float y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) y[u] = w[(long)(q + u) * c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += y[u];
+    }
+    for (; q < nchunk; ++q) s += w[(long)q * c];
     out[i] = accumulate ? out[i] + s : s;
   }
 }
@@ -1117,7 +1140,8 @@ extern "C" int rdeic_wgrad_finalize(const float* part, int32_t splits, int32_t c
 extern "C" size_t rdeic_col_sum_ws_floats(int64_t rows, int32_t c, int32_t groups) {
   if (rows <= 0 || c <= 0 || groups <= 0 || rows % groups) return 0;
   const long rpg = rows / groups;
-  return (size_t)groups * ((rpg + CS_ROWS - 1) / CS_ROWS) * c;
+  const long rpc = cs_rows(rpg);
+  return (size_t)groups * ((rpg + rpc - 1) / rpc) * c;
 }
 
 extern "C" int rdeic_col_sum(const void* x, int64_t rows, int32_t c, int32_t ld, int32_t groups, float* out,
@@ -1126,13 +1150,14 @@ extern "C" int rdeic_col_sum(const void* x, int64_t rows, int32_t c, int32_t ld,
   if (ws_floats < rdeic_col_sum_ws_floats(rows, c, groups)) return RDEIC_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
   const long rpg = rows / groups;
-  const int nchunk = (int)((rpg + CS_ROWS - 1) / CS_ROWS);
+  const long rpc = cs_rows(rpg);
+  const int nchunk = (int)((rpg + rpc - 1) / rpc);
   if (nchunk > 65535 || groups > 65535) return RDEIC_EINVAL;
   dim3 grid((c + 255) / 256, nchunk, groups);
   if (dtype == 1)
-    hipLaunchKernelGGL(col_sum_partial_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, rpg, c, ld, nchunk, ws);
+    hipLaunchKernelGGL(col_sum_partial_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, rpg, c, ld, nchunk, rpc, ws);
   else
-    hipLaunchKernelGGL(col_sum_partial_kernel<float>, grid, dim3(256), 0, s, (const float*)x, rpg, c, ld, nchunk, ws);
+    hipLaunchKernelGGL(col_sum_partial_kernel<float>, grid, dim3(256), 0, s, (const float*)x, rpg, c, ld, nchunk, rpc, ws);
   hipLaunchKernelGGL(col_sum_final_kernel, dim3(grid_1d((long)groups * c)), dim3(256), 0, s, ws, groups, nchunk, c, out,
                      accumulate);
   return launch_status();

@@ -369,7 +369,7 @@ class FineTuner:
             self.buckets.begin()
         # training needs no batch invariance anywhere: small-M / large-K convs (B=1 UNet levels, input
         # gradients) may split K (deterministic, fixed-order reduction)
-        with ops.splitk_allowed():
+        with ops.splitk_allowed(short_k=True):
             loss, d = self.losses(x_start, h, ctx, draws["t"], draws["noise"], draws["slice_noise"])
             loss.backward()
         if self.buckets is not None:
@@ -432,7 +432,7 @@ class CapturedStep:
         ft = self.ft
         ft.zero_grad()
         x_start, h = ft.get_first_stage(self.img, self.d["post_eps"])
-        with ops.splitk_allowed():
+        with ops.splitk_allowed(short_k=True):
             loss, d = ft.losses(x_start, h, self.ctx, self.d["t"], self.d["noise"], self.d["slice_noise"])
             loss.backward()
         d = {k: v.detach() for k, v in d.items()}

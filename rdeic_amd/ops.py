@@ -290,16 +290,24 @@ SPLITK_ALLOWED = False
 _SPLITK_WS: dict = {}
 
 
+SPLITK_SHORT = False  # training: also split the short-K (k-tiles >= 8) small-M layers
+
+
 class splitk_allowed:
-    """Context manager enabling split-K for small-M / large-K convs (UNet / control forward)."""
+    """Context manager enabling split-K for small-M / large-K convs (UNet / control forward).
+    short_k (the fine-tune step, B=1): also split layers with as few as 8 k-tiles."""
+
+    def __init__(self, short_k: bool = False):
+        self.short_k = short_k
 
     def __enter__(self):
-        global SPLITK_ALLOWED
-        self._prev, SPLITK_ALLOWED = SPLITK_ALLOWED, True
+        global SPLITK_ALLOWED, SPLITK_SHORT
+        self._prev = (SPLITK_ALLOWED, SPLITK_SHORT)
+        SPLITK_ALLOWED, SPLITK_SHORT = True, self.short_k or SPLITK_SHORT
 
     def __exit__(self, *exc):
-        global SPLITK_ALLOWED
-        SPLITK_ALLOWED = self._prev
+        global SPLITK_ALLOWED, SPLITK_SHORT
+        SPLITK_ALLOWED, SPLITK_SHORT = self._prev
 
 
 def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor) -> int:
@@ -313,11 +321,15 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
     if x.dtype == torch.float32:  # 64x64 fp32 tiles, 32-deep k-steps
         tiles = -(-M // 64) * -(-p.cout // 64)
         nk = -(-(p.kh * p.kw * p.cin) // 32)
+        if SPLITK_SHORT and tiles < 256 and 8 <= nk < 32:
+            return max(1, min(-(-512 // tiles), nk // 4, 16))
         if tiles >= 256 or nk < 32:
             return 1
         return max(1, min(-(-512 // tiles), nk // 8, 16))
     tiles = -(-M // 128) * -(-p.cout // 128)
     nk = -(-(p.kh * p.kw * p.cin) // 64)
+    if SPLITK_SHORT and tiles < 128 and 8 <= nk < 32:
+        return max(1, min(-(-512 // tiles), nk // 4, 8))
     if tiles >= 192 or nk < 32:
         return 1
     return max(1, min(-(-512 // tiles), nk // 16, 8))

@@ -225,7 +225,7 @@ def test_two_rank_ddp_step_equals_averaged_gradients(gpu):
         d = nchw_draws_to_nhwc(dr, "cuda")
         img = torch.from_numpy(synth_image(128, 128, 231 + r)).cuda()[None]
         x_start, h = ft.get_first_stage(img, d["post_eps"])
-        with ops.splitk_allowed():  # as FineTuner.training_step runs it
+        with ops.splitk_allowed(short_k=True):  # as FineTuner.training_step runs it
             loss, _ = ft.losses(x_start, h, synth_context().cuda(), d["t"], d["noise"], d["slice_noise"])
             loss.backward()
         gsum += ft.grad
