@@ -520,14 +520,35 @@ class AttentionFn(torch.autograd.Function):
             dq = torch.empty((batch * Lq, heads * dh), dtype=dt, device=dev)
             gemm(ds, 0, Lk, 1, k, 0, ldk, 1, dq, 0, heads * dh, m=Lq, n=dh, k=Lk, batch=nb, nb2=heads, a_bs=pl,
                  b_bs=(Lk * ldk, dh), c_bs=(Lq * heads * dh, dh))
+        # dK / dV reduce over the Lq queries into Lk x dh per head: few output tiles (d=16, the 77
+        # context tokens) and a long k. At batch 1 (the fine-tune step) they split the query range
+        # (fixed-order plane sum), so the grid fills the chip.
+        tiles = -(-Lk // 64) * -(-dh // 64) * nb
+        splits = 1
+        if batch == 1 and tiles < 512 and Lq >= 512:
+            splits = max(1, min(-(-1024 // tiles), Lq // 256))
+
+        def kv_grad(a, b, ldb):
+            out = torch.empty((batch * Lk, heads * dh), dtype=dt, device=dev)
+            if splits == 1:
+                gemm(a, 0, 1, Lk, b, 0, ldb, 1, out, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=nb, nb2=heads, a_bs=pl,
+                     b_bs=(Lq * ldb, dh), c_bs=(Lk * heads * dh, dh))
+                return out
+            ks = -(-Lq // splits)
+            ks = -(-ks // 32) * 32
+            ns = -(-Lq // ks)
+            plane = Lk * heads * dh
+            part = torch.empty((ns, plane), dtype=torch.float32, device=dev)
+            gemm(a, 0, 1, Lk, b, 0, ldb, 1, part, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=ns * heads, nb2=heads,
+                 a_bs=(0, Lq * Lk), b_bs=(0, dh), c_bs=(plane, dh), ksplit=ks)
+            tot = col_sum(part, ns, plane, plane)
+            return ops.cast(tot.view(batch * Lk, heads * dh), dt) if dt != torch.float32 else tot.view(
+                batch * Lk, heads * dh)
+
         if ctx.needs_input_grad[1]:
-            dk = torch.empty((batch * Lk, heads * dh), dtype=dt, device=dev)
-            gemm(ds, 0, 1, Lk, q, 0, ldq, 1, dk, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=nb, nb2=heads, a_bs=pl,
-                 b_bs=(Lq * ldq, dh), c_bs=(Lk * heads * dh, dh))
+            dk = kv_grad(ds, q, ldq)
         if ctx.needs_input_grad[2]:
-            dv = torch.empty((batch * Lk, heads * dh), dtype=dt, device=dev)
-            gemm(p, 0, 1, Lk, do, 0, ldo, 1, dv, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=nb, nb2=heads, a_bs=pl,
-                 b_bs=(Lq * ldo, dh), c_bs=(Lk * heads * dh, dh))
+            dv = kv_grad(p, do, ldo)
         return dq, dk, dv, None, None, None
 
 

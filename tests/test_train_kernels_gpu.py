@@ -153,11 +153,12 @@ def test_layer_norm_backward(gpu):
         assert _rel(a, b.detach()) < 1e-4
 
 
-@pytest.mark.parametrize("dh,lk", [(64, None), (16, None), (64, 77)])
-def test_attention_backward(gpu, dh, lk):
+@pytest.mark.parametrize("dh,lk,B,L", [(64, None, 2, 96), (16, None, 2, 96), (64, 77, 2, 96),
+                                       (16, None, 1, 1024), (64, 77, 1, 1024)])  # B=1: split-K dK / dV
+def test_attention_backward(gpu, dh, lk, B, L):
     from rdeic_amd import autograd as AG
     g = torch.Generator(device="cuda").manual_seed(5)
-    B, H, L = 2, 3, 96
+    H = 3
     Lk = L if lk is None else lk
     q = torch.randn((B * L, H * dh), device="cuda", generator=g)
     k = torch.randn((B * Lk, H * dh), device="cuda", generator=g)
