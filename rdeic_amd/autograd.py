@@ -475,6 +475,33 @@ def layer_norm(x, gamma, beta, eps: float = 1e-5):
 
 
 # --------------------------------------------------------------------------------------- attention
+def _heads_gemm(a, a_sm: int, a_sk: int, a_bs, b, b_sk: int, b_sn: int, b_bs, *, m: int, n: int, k: int, batch: int,
+                heads: int, dt, dev) -> torch.Tensor:
+    """Per (image, head) C = A B into a [batch * m, heads * n] token tensor (attention's P V, dS K,
+    dS^T Q, P^T dO). These have few output tiles (n = head dim) and a long k: at batch 1 (the
+    fine-tune step) k is split so the grid fills the chip, then the planes are summed in order."""
+    out = torch.empty((batch * m, heads * n), dtype=dt, device=dev)
+    tiles = -(-m // 64) * -(-n // 64) * batch * heads
+    splits = max(1, min(-(-1024 // tiles), k // 256)) if (batch == 1 and tiles < 512 and k >= 512) else 1
+    if splits == 1:
+        gemm(a, 0, a_sm, a_sk, b, 0, b_sk, b_sn, out, 0, heads * n, m=m, n=n, k=k, batch=batch * heads, nb2=heads,
+             a_bs=a_bs, b_bs=b_bs, c_bs=(m * heads * n, n))
+        return out
+    ks = -(-k // splits)
+    ks = -(-ks // 32) * 32
+    ns = -(-k // ks)
+    plane = m * heads * n
+    part = torch.empty((ns, plane), dtype=torch.float32, device=dev)
+    gemm(a, 0, a_sm, a_sk, b, 0, b_sk, b_sn, part, 0, heads * n, m=m, n=n, k=k, batch=ns * heads, nb2=heads,
+         a_bs=(0, a_bs[1]), b_bs=(0, b_bs[1]), c_bs=(plane, n), ksplit=ks)
+    if dt == torch.float32:
+        col_sum(part, ns, plane, plane, out=out.view(1, plane))
+        return out
+    tot = col_sum(part, ns, plane, plane)
+    call("rdeic_cast", tot.data_ptr(), ops.dt_code(tot), out.data_ptr(), ops.dt_code(out), plane, _sp())
+    return out
+
+
 class AttentionFn(torch.autograd.Function):
     """softmax(Q K^T * scale) V per (image, head) over 'b n (h d)' token tensors (CrossAttention.forward,
     attention.py:171-203), materialised: P is kept for the backward."""
@@ -492,9 +519,8 @@ class AttentionFn(torch.autograd.Function):
         p = torch.empty((batch, heads, Lq, Lk), dtype=dt, device=dev)
         call("rdeic_softmax_rows", s.data_ptr(), batch * heads * Lq, Lk, float(scale), p.data_ptr(), _dt(q), _sp())
         del s
-        o = torch.empty((batch * Lq, heads * dh), dtype=dt, device=dev)
-        gemm(p, 0, Lk, 1, v, 0, ldv, 1, o, 0, heads * dh, m=Lq, n=dh, k=Lk, batch=batch * heads, nb2=heads,
-             a_bs=(heads * Lq * Lk, Lq * Lk), b_bs=(Lk * ldv, dh), c_bs=(Lq * heads * dh, dh))
+        o = _heads_gemm(p, Lk, 1, (heads * Lq * Lk, Lq * Lk), v, ldv, 1, (Lk * ldv, dh), m=Lq, n=dh, k=Lk,
+                        batch=batch, heads=heads, dt=dt, dev=dev)
         ctx.dims = (batch, heads, Lq, Lk, dh, scale)
         ctx.save_for_backward(q, k, v, p)
         return o
@@ -517,38 +543,14 @@ class AttentionFn(torch.autograd.Function):
         pl = (heads * Lq * Lk, Lq * Lk)
         dq = dk = dv = None
         if ctx.needs_input_grad[0]:
-            dq = torch.empty((batch * Lq, heads * dh), dtype=dt, device=dev)
-            gemm(ds, 0, Lk, 1, k, 0, ldk, 1, dq, 0, heads * dh, m=Lq, n=dh, k=Lk, batch=nb, nb2=heads, a_bs=pl,
-                 b_bs=(Lk * ldk, dh), c_bs=(Lq * heads * dh, dh))
-        # dK / dV reduce over the Lq queries into Lk x dh per head: few output tiles (d=16, the 77
-        # context tokens) and a long k. At batch 1 (the fine-tune step) they split the query range
-        # (fixed-order plane sum), so the grid fills the chip.
-        tiles = -(-Lk // 64) * -(-dh // 64) * nb
-        splits = 1
-        if batch == 1 and tiles < 512 and Lq >= 512:
-            splits = max(1, min(-(-1024 // tiles), Lq // 256))
-
-        def kv_grad(a, b, ldb):
-            out = torch.empty((batch * Lk, heads * dh), dtype=dt, device=dev)
-            if splits == 1:
-                gemm(a, 0, 1, Lk, b, 0, ldb, 1, out, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=nb, nb2=heads, a_bs=pl,
-                     b_bs=(Lq * ldb, dh), c_bs=(Lk * heads * dh, dh))
-                return out
-            ks = -(-Lq // splits)
-            ks = -(-ks // 32) * 32
-            ns = -(-Lq // ks)
-            plane = Lk * heads * dh
-            part = torch.empty((ns, plane), dtype=torch.float32, device=dev)
-            gemm(a, 0, 1, Lk, b, 0, ldb, 1, part, 0, heads * dh, m=Lk, n=dh, k=Lq, batch=ns * heads, nb2=heads,
-                 a_bs=(0, Lq * Lk), b_bs=(0, dh), c_bs=(plane, dh), ksplit=ks)
-            tot = col_sum(part, ns, plane, plane)
-            return ops.cast(tot.view(batch * Lk, heads * dh), dt) if dt != torch.float32 else tot.view(
-                batch * Lk, heads * dh)
-
+            dq = _heads_gemm(ds, Lk, 1, pl, k, ldk, 1, (Lk * ldk, dh), m=Lq, n=dh, k=Lk, batch=batch, heads=heads,
+                             dt=dt, dev=dev)
         if ctx.needs_input_grad[1]:
-            dk = kv_grad(ds, q, ldq)
+            dk = _heads_gemm(ds, 1, Lk, pl, q, ldq, 1, (Lq * ldq, dh), m=Lk, n=dh, k=Lq, batch=batch, heads=heads,
+                             dt=dt, dev=dev)
         if ctx.needs_input_grad[2]:
-            dv = kv_grad(p, do, ldo)
+            dv = _heads_gemm(p, 1, Lk, pl, do, ldo, 1, (Lq * ldo, dh), m=Lk, n=dh, k=Lq, batch=batch, heads=heads,
+                             dt=dt, dev=dev)
         return dq, dk, dv, None, None, None
 
 
