@@ -110,14 +110,93 @@ class PackCache:
 PACKS = PackCache()
 
 
+class StepPacks:
+    """Packed forward / input-gradient weights of the TRAINABLE layers, refreshed once per step by a
+    single rdeic_pack_batch launch (in place of one pack launch per layer and use). A layer is
+    registered the first time a step packs it (packed alone then); from the next step on, refresh()
+    repacks every registered layer after the optimizer update, before the forward. Used only while
+    active (FineTuner's step), since the packs are valid only between refresh() and the update."""
+
+    def __init__(self):
+        self.entries = {}          # (id(weight), dtype, mode) -> (packed tensor, wld)
+        self.jobs = []             # (weight, packed, cout, cin, kh, kw, wld, mode)
+        self.table = None          # device job table (rdeic_pack_job[])
+        self.total = 0
+        self.dtype = None
+        self.on = False
+
+    def clear(self):
+        self.__init__()
+
+    def active(self):
+        sp = self
+
+        class _Ctx:
+            def __enter__(self_):
+                self_.prev, sp.on = sp.on, True
+
+            def __exit__(self_, *exc):
+                sp.on = self_.prev
+        return _Ctx()
+
+    def lookup(self, w, dtype, mode):
+        if not self.on:
+            return None
+        e = self.entries.get((id(w), dtype, mode))
+        if e is not None and self.table is not None and e[2]:
+            return e[0], e[1]
+        return None
+
+    def register(self, w, dtype, mode, packed, wld, cout, cin, kh, kw):
+        if not self.on or (self.dtype is not None and dtype != self.dtype):
+            return
+        key = (id(w), dtype, mode)
+        if key in self.entries:
+            return
+        self.dtype = dtype
+        self.entries[key] = (packed, wld, False)  # usable from the next refresh on
+        self.jobs.append((w, packed, cout, cin, kh, kw, wld, mode))
+        self.table = None
+
+    def refresh(self):
+        """Repack every registered layer (one launch). Builds the device job table when layers were
+        added since the last refresh (host->device copy: call outside graph capture then)."""
+        if not self.jobs:
+            return
+        if self.table is None:
+            rows, start = [], 0
+            for w, packed, cout, cin, kh, kw, wld, mode in self.jobs:
+                rows.append((w.data_ptr(), packed.data_ptr(), start, cout | (cin << 32), kh | (kw << 32),
+                             wld | (mode << 32)))
+                start += packed.numel()
+            self.total = start
+            self.table = torch.tensor(rows, dtype=torch.int64).to(self.jobs[0][1].device)
+            for k, (packed, wld, _) in list(self.entries.items()):
+                self.entries[k] = (packed, wld, True)
+        call("rdeic_pack_batch", self.table.data_ptr(), len(self.jobs), self.total,
+             int(self.dtype == torch.bfloat16), _sp())
+
+
+STEP_PACKS = StepPacks()
+
+
 def _pack_fwd(weight: torch.Tensor, bias, cfg: ConvCfg, dtype, frozen: bool) -> ops.ConvParams:
     key = (cfg.key, cfg.stride, cfg.pad, dtype)
     if frozen and cfg.key is not None and key in PACKS.fwd:
         return PACKS.fwd[key]
+    if not frozen:
+        hit = STEP_PACKS.lookup(weight, dtype, 0)
+        if hit is not None:
+            w4 = weight if weight.dim() == 4 else weight[:, :, None, None]
+            cout, cin, kh, kw = w4.shape
+            b = None if bias is None else bias.detach()
+            return ops.ConvParams(hit[0], hit[1], b, cout, cin, kh, kw, cfg.stride, cfg.pad)
     p = ops.ConvParams.pack(weight.detach(), None if bias is None else bias.detach(), stride=cfg.stride,
                             pad=cfg.pad, dtype=dtype)
     if frozen and cfg.key is not None:
         PACKS.fwd[key] = p
+    elif not frozen:
+        STEP_PACKS.register(weight, dtype, 0, p.weight, p.wld, p.cout, p.cin, p.kh, p.kw)
     return p
 
 
@@ -125,6 +204,10 @@ def _pack_dgrad(weight: torch.Tensor, dtype, frozen: bool, key) -> tuple:
     ck = (key, dtype)
     if frozen and key is not None and ck in PACKS.dgrad:
         return PACKS.dgrad[ck]
+    if not frozen:
+        hit = STEP_PACKS.lookup(weight, dtype, 1)
+        if hit is not None:
+            return hit
     w = weight.detach()
     if w.dim() == 2:
         w = w[:, :, None, None]
@@ -137,6 +220,8 @@ def _pack_dgrad(weight: torch.Tensor, dtype, frozen: bool, key) -> tuple:
     r = (packed, wld)
     if frozen and key is not None:
         PACKS.dgrad[ck] = r
+    elif not frozen:
+        STEP_PACKS.register(weight, dtype, 1, packed, wld, cout, cin, kh, kw)
     return r
 
 

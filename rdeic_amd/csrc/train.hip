@@ -259,6 +259,36 @@ __global__ void pack_dgrad_kernel(const float* __restrict__ w, int cout, int cin
   }
 }
 
+// all trainable layers' forward / input-gradient packings in one launch (rdeic_pack_batch)
+template <typename T>
+__global__ void pack_batch_kernel(const rdeic_pack_job* __restrict__ jobs, int njobs, long total) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    int lo = 0, hi = njobs - 1;  // last job with start <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].start <= i) lo = mid; else hi = mid - 1;
+    }
+    const rdeic_pack_job& j = jobs[lo];
+    const long li = i - j.start;
+    const int row = (int)(li / j.wld), kk = (int)(li - (long)row * j.wld);
+    float v = 0.f;
+    if (j.mode == 0) {  // [cout][wld], K = (ky, kx, ci)
+      if (kk < j.kh * j.kw * j.cin) {
+        const int tap = kk / j.cin, ci = kk - tap * j.cin;
+        const int ky = tap / j.kw, kx = tap - ky * j.kw;
+        v = j.w[(((long)row * j.cin + ci) * j.kh + ky) * j.kw + kx];
+      }
+    } else {  // [cin][wld], K = (ky, kx, co) of the flipped kernel
+      if (kk < j.kh * j.kw * j.cout) {
+        const int tap = kk / j.cout, co = kk - tap * j.cout;
+        const int ky = tap / j.kw, kx = tap - ky * j.kw;
+        v = j.w[(((long)co * j.cin + row) * j.kh + (j.kh - 1 - ky)) * j.kw + (j.kw - 1 - kx)];
+      }
+    }
+    reinterpret_cast<T*>(j.out)[li] = from_f32<T>(v);
+  }
+}
+
 // out[p][(ky*kw + kx)*c + ci] = x at the tap's input pixel (zero outside; up2: nearest-upsampled input)
 template <typename T>
 __global__ void im2col_kernel(const T* __restrict__ x, int n, int h, int w, int c, int ld, int kh, int kw, int stride,
@@ -1090,6 +1120,17 @@ extern "C" int rdeic_pack_conv_weight_dgrad(const float* w, int32_t cout, int32_
     hipLaunchKernelGGL(pack_dgrad_kernel<bf16>, dim3(g), dim3(256), 0, s, w, cout, cin, kh, kw, (bf16*)out, wld);
   else
     hipLaunchKernelGGL(pack_dgrad_kernel<float>, dim3(g), dim3(256), 0, s, w, cout, cin, kh, kw, (float*)out, wld);
+  return launch_status();
+}
+
+extern "C" int rdeic_pack_batch(const rdeic_pack_job* jobs, int32_t njobs, int64_t total, int32_t to_bf16,
+                                void* stream) {
+  if (!jobs || njobs <= 0 || total <= 0) return RDEIC_EINVAL;
+  const int g = grid_1d(total);
+  if (to_bf16)
+    hipLaunchKernelGGL(pack_batch_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, jobs, njobs, (long)total);
+  else
+    hipLaunchKernelGGL(pack_batch_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, jobs, njobs, (long)total);
   return launch_status();
 }
 

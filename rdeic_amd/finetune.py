@@ -77,6 +77,7 @@ class FineTuner:
             off += k
         st._packed.clear()  # inference packs of trainable layers would be stale after a step
         AG.PACKS.clear()
+        AG.STEP_PACKS.clear()
         cb = model.preprocess_model.codebook_size
         self.embed_prob = torch.zeros(cb, dtype=torch.float32, device=dev)  # VectorQuantiser buffer
         self.step_count = 0
@@ -364,12 +365,13 @@ class FineTuner:
         draws: t [B], post_eps / noise fp32 NHWC [B,h,w,4], slice_noise list of fp32 NHWC.
         Returns the loss dict (device scalars)."""
         self.zero_grad()
+        AG.STEP_PACKS.refresh()  # the trainable layers' packed weights, one launch (after the last update)
         x_start, h = self.get_first_stage(img_u8, draws["post_eps"])
         if self.buckets is not None:
             self.buckets.begin()
         # training needs no batch invariance anywhere: small-M / large-K convs (B=1 UNet levels, input
         # gradients) may split K (deterministic, fixed-order reduction)
-        with ops.splitk_allowed(short_k=True):
+        with ops.splitk_allowed(short_k=True), AG.STEP_PACKS.active():
             loss, d = self.losses(x_start, h, ctx, draws["t"], draws["noise"], draws["slice_noise"])
             loss.backward()
         if self.buckets is not None:
@@ -418,6 +420,7 @@ class CapturedStep:
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             ft.training_step(self.img, self.ctx, self.d)          # warm-up (eager)
+            AG.STEP_PACKS.refresh()  # builds the pack job table outside the capture
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
@@ -431,8 +434,9 @@ class CapturedStep:
     def _body(self):
         ft = self.ft
         ft.zero_grad()
+        AG.STEP_PACKS.refresh()
         x_start, h = ft.get_first_stage(self.img, self.d["post_eps"])
-        with ops.splitk_allowed(short_k=True):
+        with ops.splitk_allowed(short_k=True), AG.STEP_PACKS.active():
             loss, d = ft.losses(x_start, h, self.ctx, self.d["t"], self.d["noise"], self.d["slice_noise"])
             loss.backward()
         d = {k: v.detach() for k, v in d.items()}

@@ -254,3 +254,32 @@ def test_adamw_kernel_matches_torch(gpu):
         opt.step()
         AG.adamw_(p, gr, m, v, step, 2e-5)
     assert float((p - ref.detach()).abs().max()) <= 2e-7
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pack_batch_matches_single_packs(gpu, dt):
+    """rdeic_pack_batch (every trainable layer's packing in one launch) == the per-layer packers."""
+    from rdeic_amd import autograd as AG, ops
+    g = torch.Generator(device="cuda").manual_seed(9)
+    shapes = [(320, 256, 3, 3), (64, 260, 3, 3), (1280, 320, 1, 1), (16, 8, 5, 5)]
+    ws = [torch.randn(s, device="cuda", generator=g) for s in shapes]
+    sp = AG.StepPacks()
+    refs = []
+    with sp.active():
+        for w in ws:
+            p = ops.ConvParams.pack(w, None, dtype=dt)
+            sp.register(w, dt, 0, torch.empty_like(p.weight), p.wld, *w.shape)
+            refs.append(p.weight)
+            cout, cin, kh, kw = w.shape
+            wld = -(-(kh * kw * cout) // 64) * 64
+            ref_d = torch.empty((cin, wld), dtype=dt, device="cuda")
+            ops.call("rdeic_pack_conv_weight_dgrad", w.data_ptr(), cout, cin, kh, kw, ref_d.data_ptr(), wld,
+                     int(dt == torch.bfloat16), ops.stream_ptr())
+            sp.register(w, dt, 1, torch.full_like(ref_d, 7.0), wld, *w.shape)
+            refs.append(ref_d)
+        sp.refresh()
+        for w in ws:
+            for mode in (0, 1):
+                assert sp.lookup(w, dt, mode) is not None
+    for (w, packed, *_), ref in zip(sp.jobs, refs):
+        assert torch.equal(packed, ref)
