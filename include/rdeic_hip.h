@@ -337,16 +337,19 @@ int rdeic_pack_conv_weight_dgrad(const float* w, int32_t cout, int32_t cin, int3
                                  int32_t wld, int32_t to_bf16, void* stream);
 /* Every trainable layer's packing in one launch (the fine-tune step repacks its trainable weights
  * after each AdamW update): job j packs w into out as rdeic_pack_conv_weight (mode 0, [cout][wld])
- * or rdeic_pack_conv_weight_dgrad (mode 1, [cin][wld]); `start` is the job's first element in the
- * concatenation of all jobs' outputs (ascending, start[0] = 0), total = the concatenation's size.
- * jobs points to DEVICE memory. to_bf16 applies to every job. */
+ * or rdeic_pack_conv_weight_dgrad (mode 1, [cin][wld]); `start` is the job's first output ROW in the
+ * concatenation of all jobs' rows (ascending, start[0] = 0), total = the number of rows. One
+ * workgroup per row stages the row's sources in LDS: row_floats = the largest kh*kw*cin (mode 0) /
+ * kh*kw*cout (mode 1) over the jobs, at most 36864. jobs points to DEVICE memory. to_bf16 applies
+ * to every job. */
 typedef struct rdeic_pack_job {
   const float* w;
   void* out;
   int64_t start;
   int32_t cout, cin, kh, kw, wld, mode;
 } rdeic_pack_job;
-int rdeic_pack_batch(const rdeic_pack_job* jobs, int32_t njobs, int64_t total, int32_t to_bf16, void* stream);
+int rdeic_pack_batch(const rdeic_pack_job* jobs, int32_t njobs, int64_t total, int32_t row_floats, int32_t to_bf16,
+                     void* stream);
 int rdeic_zero_insert2(const void* src, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, void* dst,
                        int32_t dst_ld, int32_t dtype, void* stream);
 int rdeic_sum_pool2(const void* src, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, void* dst,

@@ -131,7 +131,7 @@ PROTOTYPES = {
     # adapter fine-tune step (train.hip)
     "rdeic_gemm_strided": (C.c_int, [C.POINTER(GemmDesc), _p]),
     "rdeic_pack_conv_weight_dgrad": (C.c_int, [_p, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
-    "rdeic_pack_batch": (C.c_int, [_p, _i32, _i64, _i32, _p]),
+    "rdeic_pack_batch": (C.c_int, [_p, _i32, _i64, _i32, _i32, _p]),
     "rdeic_zero_insert2": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
     "rdeic_sum_pool2": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
     "rdeic_pixel_unshuffle2": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),

@@ -164,16 +164,19 @@ class StepPacks:
         if not self.jobs:
             return
         if self.table is None:
-            rows, start = [], 0
+            rows, start, self.row_floats = [], 0, 1
             for w, packed, cout, cin, kh, kw, wld, mode in self.jobs:
+                self.row_floats = max(self.row_floats, kh * kw * (cin if mode == 0 else cout))
+                if self.row_floats > 36864:
+                    raise ValueError("rdeic_pack_batch: a packed row's sources exceed the LDS staging limit")
                 rows.append((w.data_ptr(), packed.data_ptr(), start, cout | (cin << 32), kh | (kw << 32),
                              wld | (mode << 32)))
-                start += packed.numel()
+                start += packed.shape[0]  # output rows
             self.total = start
             self.table = torch.tensor(rows, dtype=torch.int64).to(self.jobs[0][1].device)
             for k, (packed, wld, _) in list(self.entries.items()):
                 self.entries[k] = (packed, wld, True)
-        call("rdeic_pack_batch", self.table.data_ptr(), len(self.jobs), self.total,
+        call("rdeic_pack_batch", self.table.data_ptr(), len(self.jobs), self.total, self.row_floats,
              int(self.dtype == torch.bfloat16), _sp())
 
 

@@ -259,33 +259,48 @@ __global__ void pack_dgrad_kernel(const float* __restrict__ w, int cout, int cin
   }
 }
 
-// all trainable layers' forward / input-gradient packings in one launch (rdeic_pack_batch)
+// all trainable layers' forward / input-gradient packings in one launch (rdeic_pack_batch): one
+// workgroup per output row; the row's sources are read coalesced into LDS, then written in the
+// packed k order (LDS reads at stride kh*kw: conflict-free for the odd 1x1 / 3x3 / 5x5 filters)
+constexpr int PACK_ROW_MAX = 36864;  // floats of LDS per row (144 KB)
 template <typename T>
-__global__ void pack_batch_kernel(const rdeic_pack_job* __restrict__ jobs, int njobs, long total) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    int lo = 0, hi = njobs - 1;  // last job with start <= i
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid].start <= i) lo = mid; else hi = mid - 1;
+__global__ __launch_bounds__(256) void pack_batch_kernel(const rdeic_pack_job* __restrict__ jobs, int njobs) {
+  extern __shared__ float srow[];
+  const long r = blockIdx.x;
+  int lo = 0, hi = njobs - 1;  // last job with start <= r
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].start <= r) lo = mid; else hi = mid - 1;
+  }
+  const rdeic_pack_job j = jobs[lo];
+  const int row = (int)(r - j.start), khw = j.kh * j.kw, t = threadIdx.x;
+  T* out = reinterpret_cast<T*>(j.out) + (long)row * j.wld;
+  if (j.mode == 0) {  // row = co: w[co][ci][tap] contiguous -> out[(tap, ci)]
+    const int K = j.cin * khw;
+    const float* src = j.w + (long)row * K;
+    for (int i = t; i < K; i += 256) srow[i] = src[i];
+    __syncthreads();
+    for (int k = t; k < j.wld; k += 256) {
+      float v = 0.f;
+      if (k < K) { const int tap = k / j.cin, ci = k - tap * j.cin; v = srow[ci * khw + tap]; }
+      out[k] = from_f32<T>(v);
     }
-    const rdeic_pack_job& j = jobs[lo];
-    const long li = i - j.start;
-    const int row = (int)(li / j.wld), kk = (int)(li - (long)row * j.wld);
-    float v = 0.f;
-    if (j.mode == 0) {  // [cout][wld], K = (ky, kx, ci)
-      if (kk < j.kh * j.kw * j.cin) {
-        const int tap = kk / j.cin, ci = kk - tap * j.cin;
-        const int ky = tap / j.kw, kx = tap - ky * j.kw;
-        v = j.w[(((long)row * j.cin + ci) * j.kh + ky) * j.kw + kx];
-      }
-    } else {  // [cin][wld], K = (ky, kx, co) of the flipped kernel
-      if (kk < j.kh * j.kw * j.cout) {
-        const int tap = kk / j.cout, co = kk - tap * j.cout;
-        const int ky = tap / j.kw, kx = tap - ky * j.kw;
-        v = j.w[(((long)co * j.cin + row) * j.kh + (j.kh - 1 - ky)) * j.kw + (j.kw - 1 - kx)];
-      }
+  } else {  // row = ci: w[co][ci][tap] for every co -> out[(flipped tap, co)]
+    const int K = j.cout * khw;
+    for (int i = t; i < K; i += 256) {
+      const int co = i / khw, tap = i - co * khw;
+      srow[i] = j.w[((long)co * j.cin + row) * khw + tap];
     }
-    reinterpret_cast<T*>(j.out)[li] = from_f32<T>(v);
+    __syncthreads();
+    for (int k = t; k < j.wld; k += 256) {
+      float v = 0.f;
+      if (k < K) {
+        const int tap = k / j.cout, co = k - tap * j.cout;
+        const int ky = tap / j.kw, kx = tap - ky * j.kw;
+        v = srow[co * khw + (j.kh - 1 - ky) * j.kw + (j.kw - 1 - kx)];
+      }
+      out[k] = from_f32<T>(v);
+    }
   }
 }
 
@@ -1123,14 +1138,15 @@ extern "C" int rdeic_pack_conv_weight_dgrad(const float* w, int32_t cout, int32_
   return launch_status();
 }
 
-extern "C" int rdeic_pack_batch(const rdeic_pack_job* jobs, int32_t njobs, int64_t total, int32_t to_bf16,
-                                void* stream) {
-  if (!jobs || njobs <= 0 || total <= 0) return RDEIC_EINVAL;
-  const int g = grid_1d(total);
+extern "C" int rdeic_pack_batch(const rdeic_pack_job* jobs, int32_t njobs, int64_t total, int32_t row_floats,
+                                int32_t to_bf16, void* stream) {
+  if (!jobs || njobs <= 0 || total <= 0 || total > 0x7fffffffL || row_floats <= 0 || row_floats > PACK_ROW_MAX)
+    return RDEIC_EINVAL;
+  const size_t lds = (size_t)row_floats * sizeof(float);
   if (to_bf16)
-    hipLaunchKernelGGL(pack_batch_kernel<bf16>, dim3(g), dim3(256), 0, (hipStream_t)stream, jobs, njobs, (long)total);
+    hipLaunchKernelGGL(pack_batch_kernel<bf16>, dim3((unsigned)total), dim3(256), lds, (hipStream_t)stream, jobs, njobs);
   else
-    hipLaunchKernelGGL(pack_batch_kernel<float>, dim3(g), dim3(256), 0, (hipStream_t)stream, jobs, njobs, (long)total);
+    hipLaunchKernelGGL(pack_batch_kernel<float>, dim3((unsigned)total), dim3(256), lds, (hipStream_t)stream, jobs, njobs);
   return launch_status();
 }
 
