@@ -317,7 +317,9 @@ int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms);
  * A(i,kk) = a[i*a_sm + kk*a_sk], B(kk,j) = b[kk*b_sk + j*b_sn], C(i,j) = c[i*c_sm + j]; batch
  * z = z1*nb2 + z2 adds z1*x_bs1 + z2*x_bs2 to every operand. ksplit > 0: z1 selects the k-range
  * [z1*ksplit, (z1+1)*ksplit) instead (A/B bs1 unused; C plane z1*c_bs1), for split-K weight
- * gradients. dtype 0 fp32 / 1 bf16 inputs; c_f32 = 1 writes fp32 C. */
+ * gradients. dtype 0 fp32 / 1 bf16 inputs; c_f32 = 1 writes fp32 C. rsum (optional, NULL = off):
+ * also the row sums of A over this launch's k range, fp32 [m] at rsum + z1*rsum_bs (the bias
+ * gradient of a weight-gradient GEMM, whose A = dy^T; batch z2 must be 0). */
 typedef struct rdeic_gemm_desc {
   const void* a;
   int64_t a_bs1, a_bs2, a_sm, a_sk;
@@ -327,6 +329,8 @@ typedef struct rdeic_gemm_desc {
   int64_t c_bs1, c_bs2, c_sm;
   int32_t batch, nb2, m, n, k, ksplit, dtype, c_f32;
   float alpha, beta;
+  float* rsum;
+  int64_t rsum_bs;
 } rdeic_gemm_desc;
 int rdeic_gemm_strided(const rdeic_gemm_desc* d, void* stream);
 /* conv input gradient = the forward conv of dy with this flipped / transposed packing of the fp32
@@ -357,12 +361,14 @@ int rdeic_sum_pool2(const void* src, int32_t n, int32_t h, int32_t w, int32_t c,
 int rdeic_pixel_unshuffle2(const void* src, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, void* dst,
                            int32_t dst_ld, int32_t dtype, void* stream);
 /* weight gradient: im2col rows [p][(ky,kx,ci)] of the conv input, the split-K GEMM dy^T . cols, then
- * the sum of the split planes written (or added) in torch layout [cout][cin][kh][kw] */
+ * the sum of the split planes written (or added) in torch layout [cout][cin][kh][kw]; db (optional):
+ * the bias gradient, the split-order sum of the GEMM's row-sum planes rpart [splits][cout] (same
+ * accumulate mode) */
 int rdeic_im2col(const void* x, int32_t n, int32_t h, int32_t w, int32_t c, int32_t ld, int32_t kh, int32_t kw,
                  int32_t stride, int32_t pad_t, int32_t pad_l, int32_t ho, int32_t wo, int32_t up2, void* out,
                  int64_t out_ld, int32_t dtype, void* stream);
 int rdeic_wgrad_finalize(const float* part, int32_t splits, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
-                         float* dw, int32_t accumulate, void* stream);
+                         float* dw, int32_t accumulate, const float* rpart, float* db, void* stream);
 /* out[g][c] (+)= sum of the rows of group g (rows split into `groups` equal runs): bias / emb grads */
 size_t rdeic_col_sum_ws_floats(int64_t rows, int32_t c, int32_t groups);
 int rdeic_col_sum(const void* x, int64_t rows, int32_t c, int32_t ld, int32_t groups, float* out, int32_t accumulate,

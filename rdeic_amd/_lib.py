@@ -58,7 +58,7 @@ class GemmDesc(C.Structure):
         ("c", C.c_void_p), ("c_bs1", C.c_int64), ("c_bs2", C.c_int64), ("c_sm", C.c_int64),
         ("batch", C.c_int32), ("nb2", C.c_int32), ("m", C.c_int32), ("n", C.c_int32), ("k", C.c_int32),
         ("ksplit", C.c_int32), ("dtype", C.c_int32), ("c_f32", C.c_int32),
-        ("alpha", C.c_float), ("beta", C.c_float),
+        ("alpha", C.c_float), ("beta", C.c_float), ("rsum", C.c_void_p), ("rsum_bs", C.c_int64),
     ]
 
 
@@ -137,7 +137,7 @@ PROTOTYPES = {
     "rdeic_pixel_unshuffle2": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),
     "rdeic_im2col": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p,
                                _i64, _i32, _p]),
-    "rdeic_wgrad_finalize": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p]),
+    "rdeic_wgrad_finalize": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _p, _p, _p]),
     "rdeic_col_sum_ws_floats": (_sz, [_i64, _i32, _i32]),
     "rdeic_col_sum": (C.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i32, _p, _sz, _i32, _p]),
     "rdeic_act_fwd": (C.c_int, [_p, _i64, _i32, _i32, _p, _i32, _i32, _f, _p, _i32, _i32, _p]),

@@ -41,8 +41,9 @@ def _sp() -> int:
 
 def gemm(a, a_off: int, a_sm: int, a_sk: int, b, b_off: int, b_sk: int, b_sn: int, c, c_off: int, c_sm: int, *,
          m: int, n: int, k: int, batch: int = 1, nb2: int = 1, a_bs=(0, 0), b_bs=(0, 0), c_bs=(0, 0),
-         ksplit: int = 0, alpha: float = 1.0, beta: float = 0.0) -> None:
-    """rdeic_gemm_strided on tensors: element offsets / strides in elements of each tensor."""
+         ksplit: int = 0, alpha: float = 1.0, beta: float = 0.0, rsum=None, rsum_bs: int = 0) -> None:
+    """rdeic_gemm_strided on tensors: element offsets / strides in elements of each tensor. rsum: fp32
+    tensor receiving A's row sums per batch plane z1 (plane stride rsum_bs)."""
     if a.dtype != b.dtype:
         raise TypeError("gemm operands must share a dtype")
     if c.dtype not in (torch.float32, a.dtype):
@@ -56,6 +57,10 @@ def gemm(a, a_off: int, a_sm: int, a_sk: int, b, b_off: int, b_sk: int, b_sn: in
     d.dtype = _dt(a)
     d.c_f32 = int(c.dtype == torch.float32 and a.dtype != torch.float32)
     d.alpha, d.beta = alpha, beta
+    if rsum is not None:
+        if rsum.dtype != torch.float32:
+            raise TypeError("row sums are fp32")
+        d.rsum, d.rsum_bs = rsum.data_ptr(), rsum_bs
     call("rdeic_gemm_strided", C.byref(d), _sp())
 
 
@@ -284,7 +289,7 @@ def notify_grad(t: torch.Tensor) -> None:
 
 
 def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, cfg: ConvCfg, cout: int, cin: int, out=None,
-               accumulate: bool = False) -> torch.Tensor:
+               accumulate: bool = False, db: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fp32 [cout, cin, kh, kw] = dz^T . im2col(x) (split-K over pixels, fixed-order reduction)."""
     n, ho, wo, _ = dz.shape
     P = n * ho * wo
@@ -303,11 +308,14 @@ def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, cfg: ConvCfg, cout: int, cin: 
     ks = -(-ks // 32) * 32
     splits = -(-P // ks)
     part = torch.empty((splits, cout, K), dtype=torch.float32, device=x.device)
-    gemm(dz, 0, 1, ldz, cols, 0, b_sk, 1, part, 0, K, m=cout, n=K, k=P, batch=splits, c_bs=(cout * K, 0), ksplit=ks)
+    # db: the bias gradient (column sums of dz) as the GEMM's row sums of A = dz^T, same accumulate mode
+    rpart = torch.empty((splits, cout), dtype=torch.float32, device=x.device) if db is not None else None
+    gemm(dz, 0, 1, ldz, cols, 0, b_sk, 1, part, 0, K, m=cout, n=K, k=P, batch=splits, c_bs=(cout * K, 0), ksplit=ks,
+         rsum=rpart, rsum_bs=cout)
     if out is None:
         out = torch.empty((cout, cin, cfg.kh, cfg.kw), dtype=torch.float32, device=x.device)
     call("rdeic_wgrad_finalize", part.data_ptr(), splits, cout, cin, cfg.kh, cfg.kw, out.data_ptr(), int(accumulate),
-         _sp())
+         None if db is None else rpart.data_ptr(), None if db is None else db.data_ptr(), _sp())
     return out
 
 
@@ -357,17 +365,20 @@ def _conv_backward(x, weight, z, dout, cfg: ConvCfg, in_hw, need_x, need_w, need
     dx = dw = db = demb = None
     if need_x:
         dx = conv_dgrad(dz, weight, cfg, in_hw, frozen=not weight.requires_grad)
+    gvw = direct_grad_view(weight) if need_w and getattr(weight, "_rdeic_uses", 0) > 0 else None
+    gvb = direct_grad_view(bias) if need_b else None  # bias is passed only when counted in the forward
+    fuse_b = gvw is not None and gvb is not None  # bias gradient from the weight-gradient GEMM's row sums
     if need_w:
-        gv = direct_grad_view(weight) if getattr(weight, "_rdeic_uses", 0) > 0 else None
-        if gv is not None:
-            conv_wgrad(x, dz, cfg, cout, cin, out=gv, accumulate=True)
+        if gvw is not None:
+            conv_wgrad(x, dz, cfg, cout, cin, out=gvw, accumulate=True, db=gvb if fuse_b else None)
             notify_grad(weight)
         else:
             dw = conv_wgrad(x, dz, cfg, cout, cin).view(weight.shape)
     if need_b:
-        gv = direct_grad_view(bias)  # bias is passed only when counted in the forward
-        if gv is not None:
-            col_sum(dz, n * ho * wo, cout, cout, out=gv.view(1, cout), accumulate=True)
+        if fuse_b:
+            notify_grad(bias)
+        elif gvb is not None:
+            col_sum(dz, n * ho * wo, cout, cout, out=gvb.view(1, cout), accumulate=True)
             notify_grad(bias)
         else:
             db = col_sum(dz, n * ho * wo, cout, cout).view(cout)

@@ -42,6 +42,8 @@ struct GemmArgs {
   long c_bs1, c_bs2, c_sm;
   int nb2, m, n, k, ksplit, c_f32;
   float alpha, beta;
+  float* rsum;  // optional row sums of A (see rdeic_gemm_desc)
+  long rsum_bs;
 };
 
 constexpr int GBK = 32;
@@ -165,6 +167,12 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int wm = (wave >> 1) * (TB / 2), wn = (wave & 1) * (TB / 2);
+  // row sums of A (bias gradient): the n-column-0 blocks' left waves run one extra MFMA per A
+  // fragment against a ones operand
+  const bool rs = g.rsum != nullptr && blockIdx.x == 0 && (wave & 1) == 0;
+  f32x4 racc[TF];
+#pragma unroll
+  for (int i = 0; i < TF; ++i) racc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   load(0);
   for (long k0 = 0; k0 < klen; k0 += GBK) {
     __syncthreads();
@@ -189,6 +197,13 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
       for (int i = 0; i < TF; ++i)
 #pragma unroll
         for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (rs) {
+        bf16x8 ones;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+#pragma unroll
+        for (int i = 0; i < TF; ++i) racc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, racc[i], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int s = 0; s < GBK / 4; ++s) {
@@ -203,8 +218,22 @@ __global__ __launch_bounds__(256) void gemm_strided_kernel(GemmArgs g) {
         for (int i = 0; i < TF; ++i)
 #pragma unroll
           for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if (rs) {
+#pragma unroll
+          for (int i = 0; i < TF; ++i) racc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], 1.0f, racc[i], 0, 0, 0);
+        }
       }
     }
+  }
+  if (rs && lr == 0) {  // every column of racc holds the row sum; lanes of column 0 write 4 rows each
+    float* rp = g.rsum + (long)z1 * g.rsum_bs;
+#pragma unroll
+    for (int i = 0; i < TF; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int mm = m0 + wm + 16 * i + 4 * lg + r;
+        if (mm < g.m) rp[mm] = racc[i][r];
+      }
   }
   const long coff = z1 * g.c_bs1 + z2 * g.c_bs2;
 #pragma unroll
@@ -381,9 +410,17 @@ __global__ void pixel_unshuffle2_kernel(const T* __restrict__ src, int n, int h,
 
 // dw[co][ci][ky][kx] (+)= sum_s part[s][co][(ky*kw + kx)*cin + ci]
 __global__ void wgrad_finalize_kernel(const float* __restrict__ part, int splits, int cout, int cin, int kh, int kw,
-                                      float* __restrict__ dw, int accumulate) {
+                                      float* __restrict__ dw, int accumulate, const float* __restrict__ rpart,
+                                      float* __restrict__ db) {
   const int K = kh * kw * cin;
   const long total = (long)cout * K;
+  if (db && blockIdx.x == 0) {  // bias gradient: the GEMM's row-sum planes, summed in split order
+    for (int co = threadIdx.x; co < cout; co += 256) {
+      float s = 0.f;
+      for (int sp = 0; sp < splits; ++sp) s += rpart[(long)sp * cout + co];
+      db[co] = accumulate ? db[co] + s : s;
+    }
+  }
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int co = (int)(i / K), kk = (int)(i - (long)co * K);
     float s = 0.f;
@@ -1108,7 +1145,8 @@ extern "C" int rdeic_gemm_strided(const rdeic_gemm_desc* d, void* stream) {
   g.c = d->c; g.c_bs1 = d->c_bs1; g.c_bs2 = d->c_bs2; g.c_sm = d->c_sm;
   g.nb2 = d->nb2; g.m = d->m; g.n = d->n; g.k = d->k; g.ksplit = d->ksplit; g.c_f32 = d->c_f32;
   g.alpha = d->alpha; g.beta = d->beta;
-  if (d->batch > 65535) return RDEIC_EINVAL;
+  g.rsum = d->rsum; g.rsum_bs = d->rsum_bs;
+  if (d->batch > 65535 || (d->rsum && d->nb2 != 1)) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const double flops = 2.0 * d->m * d->n * (d->ksplit > 0 ? (double)d->k : (double)d->k * (d->batch / d->nb2)) * d->nb2;
   ProfScope ps(s, RDEIC_PROF_GEMM, flops);
@@ -1187,10 +1225,12 @@ RDEIC_LAYOUT_OP(rdeic_pixel_unshuffle2, pixel_unshuffle2_kernel, 4)
 #undef RDEIC_LAYOUT_OP
 
 extern "C" int rdeic_wgrad_finalize(const float* part, int32_t splits, int32_t cout, int32_t cin, int32_t kh,
-                                    int32_t kw, float* dw, int32_t accumulate, void* stream) {
-  if (!part || !dw || splits <= 0 || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return RDEIC_EINVAL;
+                                    int32_t kw, float* dw, int32_t accumulate, const float* rpart, float* db,
+                                    void* stream) {
+  if (!part || !dw || splits <= 0 || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0 || (db && !rpart))
+    return RDEIC_EINVAL;
   hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(grid_1d((long)cout * kh * kw * cin)), dim3(256), 0,
-                     (hipStream_t)stream, part, splits, cout, cin, kh, kw, dw, accumulate);
+                     (hipStream_t)stream, part, splits, cout, cin, kh, kw, dw, accumulate, rpart, db);
   return launch_status();
 }
 

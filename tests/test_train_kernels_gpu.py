@@ -47,9 +47,11 @@ def test_gemm_strided(gpu, dt, layout, shape):
     # split-K planes sum to the product
     ks = -(-k // planes)
     P = torch.empty((planes, m, n), device="cuda", dtype=torch.float32)
+    R = torch.empty((planes, m), device="cuda", dtype=torch.float32)  # row sums of A (bias gradients)
     AG.gemm(a_st[0], 0, a_sm, a_sk, b_st[0], 0, b_sk, b_sn, P, 0, n, m=m, n=n, k=k, batch=planes, c_bs=(m * n, 0),
-            ksplit=ks)
+            ksplit=ks, rsum=R, rsum_bs=m)
     assert _rel(P.sum(0), ref[0]) < tol
+    assert _rel(R.sum(0), A[0].to(dt).float().sum(1)) < tol
 
 
 CONV_CASES = [
