@@ -33,7 +33,7 @@ SHAPES = [
     ("lin1280x1280", 1, 4096, 1, 1280, 0, 1280, 1, 1, 0, None),
     ("tail3x20x20_128to192", 3, 20, 20, 128, 0, 192, 3, 1, 0, None),
 ]
-TILES = (-1, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34)
+TILES = (-1, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35)
 
 
 def bench(fn, reps):
