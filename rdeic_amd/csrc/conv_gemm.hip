@@ -144,35 +144,8 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
   // block) and (BM / 64) * BN <= NT; the host enables it only for such tiles (stats_tile_ok).
   const bool st = a.gn_part != nullptr;
   float sg[4] = {0.f, 0.f, 0.f, 0.f}, qg[4] = {0.f, 0.f, 0.f, 0.f};
-  // Operand prefetch: a thread's chunks of one pass are c = tid + i * NT. Their bf16 residual
-  // vectors are loaded BEFORE the accumulators are parked, so the HBM latency hides behind the two
-  // barriers and the LDS round trip instead of stalling the chunk loop; when NT is a multiple of
-  // CPR every chunk of the thread has the same 8 output channels, so the bias is loaded once.
-  constexpr int NCH = (PR * CPR + NT - 1) / NT;
-  constexpr bool FIXCC = (NT % CPR) == 0;
-  const bool rpf = a.res && !of32;
-  float bias_c[8];
-  if constexpr (FIXCC) {
-    const int nn = n0 + (tid % CPR) * 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bias_c[e] = (a.bias && nn < a.cout) ? a.bias[nn + e] : 0.f;
-  }
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    uint4 rv_pre[NCH];
-    if (rpf) {
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        const int c = tid + i * NT;
-        if (c >= PR * CPR) break;
-        const int pr = c / CPR, cc = c - pr * CPR;
-        const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
-        const int m = m0 + wmr * WTM + p * (WTM / P) + wr;
-        const int nn = n0 + cc * 8;
-        if (m < a.M && nn < a.cout)
-          rv_pre[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.res) + (long)m * a.res_ld + nn);
-      }
-    }
     __syncthreads();
 #pragma unroll
     for (int ii = 0; ii < HM; ++ii)
@@ -183,10 +156,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
         for (int j = 0; j < TN; ++j) L[pr * SDW + wn * WTN + j * 16 + lr] = acc[p * HM + ii][j][r];
       }
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = tid + i * NT;
-      if (c >= PR * CPR) break;
+    for (int c = tid; c < PR * CPR; c += NT) {
       const int pr = c / CPR, cc = c - pr * CPR;
       // pass-local row pr -> wave row block wm' = pr / (WTM/P), row within = pr % (WTM/P)
       const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
@@ -199,7 +169,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
       v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
       if (a.bias) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += FIXCC ? bias_c[e] : a.bias[nn + e];
+        for (int e = 0; e < 8; ++e) v[e] += a.bias[nn + e];
       }
       if (a.emb) {
         const float* em = a.emb + (long)(m / hw_o) * a.emb_ld + nn;
@@ -229,7 +199,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
           v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
         } else {
           bf16 rv[8];
-          *reinterpret_cast<uint4*>(rv) = rv_pre[i];
+          *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.res) + (long)m * a.res_ld + nn);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += to_f32(rv[e]);
         }

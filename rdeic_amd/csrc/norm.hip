@@ -468,11 +468,25 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const float* __r
     const int R = reinterpret_cast<const int*>(p)[0];
     const int T = hw / R, nch = hi - lo;
     const float* q = p + 4 + ((long)img * T * cs + (lo - base)) * 2;
-    for (int i = t; i < T * nch; i += 256) {
-      const int tt = i / nch, j = i - tt * nch;
-      const float* e = q + ((long)tt * cs + j) * 2;
-      S += (double)e[0];
-      Q += (double)e[1];
+    // thread t sums the row blocks t, t + 256, ...: each one's nch (sum, sum of squares) pairs are
+    // contiguous, read as 16-byte vectors when the channel count and the alignment allow
+    const bool vec = (nch & 1) == 0 && (cs & 1) == 0 && (((uintptr_t)q) & 15) == 0;
+    for (int tt = t; tt < T; tt += 256) {
+      const float* e = q + (long)tt * cs * 2;
+      if (vec) {
+        for (int j = 0; j < nch; j += 2) {
+          const float4 v = *reinterpret_cast<const float4*>(e + 2 * j);
+          S += (double)v.x;
+          Q += (double)v.y;
+          S += (double)v.z;
+          Q += (double)v.w;
+        }
+      } else {
+        for (int j = 0; j < nch; ++j) {
+          S += (double)e[2 * j];
+          Q += (double)e[2 * j + 1];
+        }
+      }
     }
   }
   S = block_sum256_d(S, red);

@@ -581,9 +581,10 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
 
 
 # Score-buffer budget of the single-head (VAE, d=512) attention: the fp32 scores of one query
-# chunk never exceed it, so the buffer is O(chunk x L), not O(B x L^2) (at 1024x1024 one image's
-# full score matrix alone would be 16384^2 x 4 B = 1 GiB).
-SCORE_BUDGET_BYTES = 1 << 30
+# chunk never exceed it, so the buffer is O(chunk x L), not O(B x L^2). At 1024x1024 one image's
+# full score matrix would be 16384^2 x 4 B = 1 GiB: it runs as 4 query-row chunks of 4096 rows.
+# At 512x512 (64 MiB per image) a chunk holds 4 images.
+SCORE_BUDGET_BYTES = 1 << 28
 
 
 def attention_single_head_materialized(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, *,
