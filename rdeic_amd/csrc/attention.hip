@@ -852,10 +852,187 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
   }
 }
 
+// ============================================================================================
+// bf16 single-head attention with head dim 512 (the VAE AttnBlock, model.py:181-205), flash form:
+// no score matrix in HBM. One 256-thread block = 4 waves x 16 queries (O^T and Q^T of 16 queries
+// take ~200 VGPRs: one wave per SIMD); 32-key K and V tiles (1 KB
+// rows) move L2 -> LDS by LDS-DMA into a 2-deep ring (2 x 64 KB), one raw s_barrier per tile.
+// Per wave and tile: S^T = K Q^T (Q^T fragments held in registers, 16 x 32-d slices), online
+// softmax in the exp2 domain with the deferred-max rescale of attn64 (threshold 8), row sums on the
+// matrix core (ones operand), O^T += V^T P^T over 32 d-blocks with V^T read by ds_read_b64_tr_b16.
+// Swizzles (applied on the DMA source side): K chunk c of row r at slot c ^ (r & 15) (conflict-free
+// ds_read_b128 fragment rows), V chunk c at slot c ^ ((r & 7) << 1) (conflict-free transposed
+// reads). Requires lk % 32 == 0 (L = H * W of the VAE latent grid).
+// ============================================================================================
+constexpr int A512_Q = 64, A512_KT = 32, A512_TILE = A512_KT * 1024, A512_STAGE = 2 * A512_TILE;
+
+__global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
+                                                      int ldk, const bf16* __restrict__ v, int ldv,
+                                                      bf16* __restrict__ o, int ldo, int lq, int lk,
+                                                      float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // 2 x (K tile | V tile)
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, g = lane >> 4;
+  const bf16* qb = q + (long)b * lq * ldq;
+  const bf16* kb = k + (long)b * lk * ldk;
+  const bf16* vb = v + (long)b * lk * ldv;
+  const int q0 = blockIdx.x * A512_Q + wave * 16;
+
+  // Q^T fragments (B operand, 32 d x 16 queries): lane (query lr, k-group g) holds d 32hd + 8g .. +8
+  bf16x8 qf[16];
+  {
+    const int qq = q0 + lr;
+    const bf16* qr = qb + (long)min(qq, lq - 1) * ldq + 8 * g;
+#pragma unroll
+    for (int hd = 0; hd < 16; ++hd) {
+      bf16x8 z = *reinterpret_cast<const bf16x8*>(qr + 32 * hd);
+      if (qq >= lq) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
+      }
+      qf[hd] = z;
+    }
+  }
+
+  const __amdgpu_buffer_rsrc_t rsk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)kb, (short)0, (int)(((long)(lk - 1) * ldk + 512) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)vb, (short)0, (int)(((long)(lk - 1) * ldv + 512) * 2), 0x00020000);
+  // DMA: one wave-instruction moves one 1 KB key row; wave w fills K rows 8w..8w+7 and V rows 8w..8w+7
+  auto issue = [&](int kt, int slot) {
+    char* sb = lds + slot * A512_STAGE;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int row = 8 * wave + j;
+      const unsigned key = (unsigned)(kt * A512_KT + row);
+      const unsigned kc = (unsigned)(lane ^ (row & 15)), vc = (unsigned)(lane ^ ((row & 7) << 1));
+      attn_dma16(rsk, sb + row * 1024, key * (unsigned)(ldk * 2) + kc * 16u);
+      attn_dma16(rsv, sb + A512_TILE + row * 1024, key * (unsigned)(ldv * 2) + vc * 16u);
+    }
+  };
+
+  f32x4 oacc[32];
+#pragma unroll
+  for (int dt = 0; dt < 32; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY;
+  float lsum = 0.f;  // this lane's share of its query's row sum (the 8 keys it holds per tile)
+  const int vq = lr >> 2, vp = lr & 3;  // transposed read: block row vq, column group vp
+
+  const int ntiles = lk / A512_KT;
+  issue(0, 0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    attn_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < ntiles) issue(kt + 1, (kt + 1) & 1);
+    const char* Kt = lds + (kt & 1) * A512_STAGE;
+    const char* Vt = Kt + A512_TILE;
+    // S^T (32 keys x 16 queries): st[kb] rows = keys 16kb + 4g + i, column = query lr
+    // one wave per SIMD: the compiler hoists the K fragment reads of all 16 slices (latency hiding
+    // by registers, ~430 of the 512 available)
+    f32x4 st[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    auto kfrag = [&](int hd, int kb2) {
+      const int row = 16 * kb2 + lr;
+      return *reinterpret_cast<const bf16x8*>(Kt + row * 1024 + (((4 * hd + g) ^ (row & 15)) * 16));
+    };
+#pragma unroll
+    for (int hd = 0; hd < 16; ++hd) {
+      const bf16x8 k0 = kfrag(hd, 0), k1 = kfrag(hd, 1);
+      st[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[hd], st[0], 0, 0, 0);
+      st[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[hd], st[1], 0, 0, 0);
+    }
+    float mx = st[0][0];
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[kb2][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float ms = mx * scale_log2;
+    float alpha = 1.f;
+    bool rescale = false;
+    if (ms > m_run + 8.f) {
+      alpha = __builtin_amdgcn_exp2f(m_run - ms);
+      m_run = ms;
+      rescale = true;
+    }
+    const float nm = -m_run;
+    bf16x8 pf;  // P^T (B operand): k index j <-> key 16 (j >> 2) + 4g + (j & 3)
+    float ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      pf[j] = (bf16)__builtin_amdgcn_exp2f(fmaf(st[j >> 2][j & 3], scale_log2, nm));
+      ps += (float)pf[j];  // the bf16 probabilities that enter O
+    }
+    if (__any(rescale)) {
+#pragma unroll
+      for (int dt = 0; dt < 32; ++dt) oacc[dt] *= alpha;
+    }
+    lsum = lsum * alpha + ps;
+    // O^T[dt] (16 d x 16 queries) += V^T (16 d x 32 keys) P^T; lane (d = 16dt + lr, g) reads
+    // V[keys 4g + vq (+16)][d], two transposed reads per dt, issued one d-pair ahead
+    const int row0 = 4 * g + vq;  // rows row0 and row0 + 16 share the swizzle ((r & 7) << 1)
+    const unsigned vbase = (unsigned)(uintptr_t)(lds_vptr_t)Vt + row0 * 1024 + (vp & 1) * 8;
+    const int swz = (row0 & 7) << 1;
+    auto vaddr = [&](int dt) { return vbase + (unsigned)(((2 * dt + (vp >> 1)) ^ swz) * 16); };
+    constexpr int VD = 4;  // d-blocks of V^T reads in flight (ring of VD; counted lgkmcnt)
+    v4s vt[VD][2];         // [ring slot][lo / hi rows]
+#pragma unroll
+    for (int u = 0; u < VD - 1; ++u) {
+      vt[u][0] = ds_read_tr16_off<0>(vaddr(u));
+      vt[u][1] = ds_read_tr16_off<16 * 1024>(vaddr(u));
+    }
+#pragma unroll
+    for (int dt = 0; dt < 32; ++dt) {
+      const int cb = dt % VD;
+      if (dt + VD - 1 < 32) {
+        const unsigned a = vaddr(dt + VD - 1);
+        vt[(dt + VD - 1) % VD][0] = ds_read_tr16_off<0>(a);
+        vt[(dt + VD - 1) % VD][1] = ds_read_tr16_off<16 * 1024>(a);
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * (VD - 1)) : "memory");
+      } else if (dt + 2 < 32) {
+        asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+      } else if (dt + 1 < 32) {
+        asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      const v4s both[2] = {vt[cb][0], vt[cb][1]};
+      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(both);
+      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[dt], 0, 0, 0);
+    }
+  }
+  float l = lsum;
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  const int qq = q0 + lr;
+  if (qq < lq) {
+    bf16* orow = o + ((long)b * lq + qq) * ldo;
+#pragma unroll
+    for (int dt = 0; dt < 32; ++dt) {
+      bf16x4 ov;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ov[i] = (bf16)(oacc[dt][i] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = ov;
+    }
+  }
+}
+
 template <typename T>
 int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo, int batch,
                 int heads, int lq, int lk, int dh, float scale, int kv_bcast, hipStream_t s) {
   if constexpr (sizeof(T) == 2) {
+    if (dh == 512) {
+      if (heads != 1 || kv_bcast || lk % A512_KT || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4 || ((uintptr_t)o) % 8 ||
+          (long)(lk - 1) * (ldk > ldv ? ldk : ldv) * 2 + 1024 >= (1l << 31))
+        return RDEIC_EINVAL;
+      dim3 grid((lq + A512_Q - 1) / A512_Q, batch);
+      hipLaunchKernelGGL(attn512_kernel, grid, dim3(256), 2 * A512_STAGE, s, (const bf16*)q, ldq, (const bf16*)k, ldk,
+                         (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f);
+      return launch_status();
+    }
     if (dh == 64 && rdeic_g_attn64 == 2 && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 &&
         (long)(lk - 1) * (ldk > ldv ? ldk : ldv) * 2 + 128 < (1l << 31)) {
       dim3 grid((lq + A64_Q - 1) / A64_Q, batch * heads);

@@ -580,6 +580,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
     return out
 
 
+# VAE AttnBlock in bf16 on the flash kernel (rdeic_attention, dh = 512); False: the materialised path
+VAE_FLASH_ATTENTION = True
+
 # Score-buffer budget of the single-head (VAE, d=512) attention: the fp32 scores of one query
 # chunk never exceed it, so the buffer is O(chunk x L), not O(B x L^2). At 1024x1024 one image's
 # full score matrix would be 16384^2 x 4 B = 1 GiB: it runs as 4 query-row chunks of 4096 rows.

@@ -110,8 +110,13 @@ class AutoencoderKL:
         qkv = ops.conv2d(x, s.conv_cat([pre + ".q", pre + ".k", pre + ".v"]), gn=ab, gn_silu=False)
         qkv = qkv.view(B * L, 3 * C)
         o = torch.empty((B * L, C), dtype=x.dtype, device=x.device)
-        ops.attention_single_head_materialized(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch=B, length=L,
-                                               dim=C, scale=int(C) ** (-0.5))
+        if x.dtype == torch.bfloat16 and C == 512 and L % 32 == 0 and ops.VAE_FLASH_ATTENTION:
+            # flash kernel (attention.hip attn512_kernel): no score matrix in HBM
+            ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch=B, heads=1, lq=L, lk=L, dh=C,
+                          scale=int(C) ** (-0.5))
+        else:  # fp32 parity mode: the materialised GEMM -> softmax -> GEMM (reference op order)
+            ops.attention_single_head_materialized(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch=B,
+                                                   length=L, dim=C, scale=int(C) ** (-0.5))
         out = ops.linear(o, s.conv(pre + ".proj_out"), res=x.contiguous().view(B * L, C), stats_hw=L)
         return ops.tokens_to_nhwc(out, B, H, W_)
 

@@ -30,3 +30,29 @@ def test_single_head_attention_chunked_is_exact(gpu, dtype):
         @ v.float().view(B, L, C)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
     torch.testing.assert_close(full.float().view(B, L, C), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("B,L,spread", [(2, 1024, 1.0), (1, 4096, 1.0), (2, 256, 6.0), (1, 96, 1.0)])
+def test_flash_d512_matches_fp32_reference(gpu, B, L, spread):
+    """The flash kernel (rdeic_attention, dh = 512, bf16): no score buffer; against torch fp32 on the
+    same bf16 inputs, on the AttnBlock's [B*L, 3C] qkv layout (row stride 3C). spread > 1 gives
+    large logits so the deferred-max rescale path runs; L = 96 has a partial 64-query block."""
+    from rdeic_amd import ops
+    C = 512
+    g = torch.Generator(device="cuda").manual_seed(L)
+    qkv = (torch.randn(B * L, 3 * C, device="cuda", generator=g) * spread).to(torch.bfloat16)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    scale = C ** -0.5
+    out = torch.empty(B * L, C, dtype=torch.bfloat16, device="cuda")
+    ops.attention(q, k, v, out, batch=B, heads=1, lq=L, lk=L, dh=C, scale=scale)
+    torch.cuda.synchronize()
+    qf, kf, vf = (t.float().reshape(B, L, C) for t in (q, k, v))
+    ref = torch.softmax((qf @ kf.transpose(1, 2)) * scale, -1) @ vf
+    err = (out.float().view(B, L, C) - ref).abs()
+    # bf16 probabilities (P) and bf16 output: ~1e-2 relative to the output scale
+    assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max().item()
+    assert err.mean().item() < 2e-3 * max(1.0, ref.abs().max().item()), err.mean().item()
+    if spread == 1.0 and L % 64 == 0:
+        mat = torch.empty_like(out)
+        ops.attention_single_head_materialized(q, k, v, mat, batch=B, length=L, dim=C, scale=scale)
+        assert (mat.float() - out.float()).abs().max().item() < 2e-2
