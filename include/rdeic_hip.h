@@ -145,12 +145,14 @@ int rdeic_layernorm(const void* x, int32_t rows, int32_t c, int32_t ld, const fl
  * softmax(Q K^T * scale) V per (batch, head); Q [b][lq][ldq] with head h at columns
  * h*dh..h*dh+dh-1 (same for K/V/O), i.e. the reference's 'b n (h d)' layout.
  * dh in {16, 32, 64}; any lq, lk >= 1. kv_bcast = 1: K/V hold a single batch shared by all
- * `batch` query batches (the one text context of the cross-attention). */
+ * `batch` query batches (the one text context of the cross-attention).
+ * dh = 512 (bf16, heads = 1, lk % 32 == 0, no kv_bcast): the VAE AttnBlock (model.py:181-205) as a
+ * flash kernel, no score matrix in memory. */
 int rdeic_attention(const void* q, int32_t ldq, const void* k, int32_t ldk, const void* v, int32_t ldv,
                     void* o, int32_t ldo, int32_t batch, int32_t heads, int32_t lq, int32_t lk, int32_t dh,
                     float scale, int32_t kv_bcast, int32_t dtype, void* stream);
-/* materialised-attention helpers (VAE d=512 single-head path): row softmax of s*scale -> p,
- * and batched 2-D transpose. */
+/* materialised-attention helpers (VAE d=512 single-head path in fp32 parity mode): row softmax of
+ * s*scale -> p, and batched 2-D transpose. */
 int rdeic_softmax_rows(const float* s, int64_t rows, int32_t cols, float scale, void* p, int32_t dtype, void* stream);
 int rdeic_transpose(const void* in, int32_t rows, int32_t cols, int32_t ldin, void* out, int32_t ldout,
                     int32_t batch, int64_t in_bs, int64_t out_bs, int32_t dtype, void* stream);
@@ -303,6 +305,7 @@ int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row);
 #define RDEIC_PROF_GN_STATS 3    /* rdeic_groupnorm_stats: bytes read */
 #define RDEIC_PROF_GN_APPLY 4    /* rdeic_groupnorm_apply: bytes read + written */
 #define RDEIC_PROF_GEMM 5        /* rdeic_gemm_strided (training backward / attention): 2*M*N*K*batch FLOPs */
+#define RDEIC_PROF_ATTN_D512 6   /* rdeic_attention, head dim 512 (VAE AttnBlock flash kernel): 4*B*Lq*Lk*512 FLOPs */
 int rdeic_prof_start(int32_t capacity, int32_t every);
 int rdeic_prof_stop(void);
 int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms);

@@ -1093,7 +1093,8 @@ extern "C" int rdeic_attention(const void* q, int32_t ldq, const void* k, int32_
   if (ldq % epc || ldk % epc || ldv % epc || ((uintptr_t)k) % 16 || ((uintptr_t)v) % 16 || ((uintptr_t)q) % 16)
     return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  ProfScope ps(s, dh >= 64 ? RDEIC_PROF_ATTN : RDEIC_PROF_ATTN_SMALL, 4.0 * batch * heads * (double)lq * lk * dh);
+  ProfScope ps(s, dh == 512 ? RDEIC_PROF_ATTN_D512 : dh >= 64 ? RDEIC_PROF_ATTN : RDEIC_PROF_ATTN_SMALL,
+               4.0 * batch * heads * (double)lq * lk * dh);
   if (dtype == 1) return launch_attn<bf16>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
   return launch_attn<float>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
 }

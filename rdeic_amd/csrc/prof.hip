@@ -23,7 +23,7 @@ std::mutex g_mu;
 
 double always_threshold(int kind) {
   // FLOP for the conv / attention kinds, bytes for the GroupNorm kinds
-  return (kind <= RDEIC_PROF_ATTN_SMALL || kind == RDEIC_PROF_GEMM) ? 50e9 : 64e6;
+  return (kind <= RDEIC_PROF_ATTN_SMALL || kind == RDEIC_PROF_GEMM || kind == RDEIC_PROF_ATTN_D512) ? 50e9 : 64e6;
 }
 }  // namespace
 

@@ -380,7 +380,8 @@ def record_profile(tag, ev0, ev1):
         PROFILE_OTHER.setdefault(kind, []).append((work, ev0, ev1))
 
 
-PROF_KINDS = {"conv": 0, "attention": 1, "attention_dh16": 2, "gn_stats": 3, "gn_apply": 4, "gemm": 5}
+PROF_KINDS = {"conv": 0, "attention": 1, "attention_dh16": 2, "gn_stats": 3, "gn_apply": 4, "gemm": 5,
+              "attention_d512": 6}
 
 
 def prof_start(capacity: int = 65536, every: int = 1) -> None:
@@ -573,7 +574,8 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tens
               lq: int, lk: int, dh: int, scale: float, kv_bcast: bool = False) -> torch.Tensor:
     """Flash attention over [batch*lq, heads*dh]-layout projections (row strides from the tensors).
     kv_bcast: K/V hold one batch shared by every query batch."""
-    _launch(("attention" if dh >= 64 else "attention_dh%d" % dh, 4.0 * batch * heads * lq * lk * dh, None),
+    _launch(("attention_d512" if dh == 512 else "attention" if dh >= 64 else "attention_dh%d" % dh,
+             4.0 * batch * heads * lq * lk * dh, None),
             "rdeic_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(),
             v.stride(0), out.data_ptr(), out.stride(0), batch, heads, lq, lk, dh, float(scale),
             int(kv_bcast), dt_code(q), stream_ptr())
