@@ -332,7 +332,10 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
         return max(1, min(-(-512 // tiles), nk // 4, 8))
     if tiles >= 192 or nk < 32:
         return 1
-    return max(1, min(-(-512 // tiles), nk // 16, 8))
+    # tiles x splits within the 512 co-resident 128x128 blocks (2 per CU): one more split past that
+    # starts a second round of blocks (tools/splitk_bench.py, UNet 8x8 level: 7 splits 419 / 503 TF,
+    # 6 splits 528 / 674 TF for the 1280 / 2560-channel inputs)
+    return max(1, min(512 // tiles, nk // 16, 8))
 
 
 _SPLITK_KEEP: list = []  # every workspace ever handed out: recorded launch plans hold their pointers

@@ -1,0 +1,53 @@
+"""Split-K A/B on the UNet's small-grid 3x3 layers (bf16, B=16): the table's tile without split
+against forced k-split counts (split-K runs on the heuristic DMA tile, fixed-order reduce)."""
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rdeic_amd import ops  # noqa: E402
+
+SHAPES = [("unet640@32", 16, 32, 32, 640, 640, (2, 3, 4, 6)), ("unet1280@16", 16, 16, 16, 1280, 1280, (2, 3)),
+          ("unet1280@8", 16, 8, 8, 1280, 1280, (3, 4, 5, 6, 7, 8)), ("unet2560@8", 16, 8, 8, 2560, 1280, (4, 6, 7, 8))]
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = float("inf")
+    for _ in range(3):
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / reps)
+    return best
+
+
+def main():
+    orig = ops._splitk_count
+    for name, B, H, W, cin, cout, splits in SHAPES:
+        x = torch.randn(B, H, W, cin, device="cuda").to(torch.bfloat16)
+        w = torch.randn(cout, cin, 3, 3, device="cuda") / math.sqrt(cin * 9)
+        p = ops.ConvParams.pack(w, torch.randn(cout, device="cuda"), stride=1, pad=1)
+        emb = torch.randn(B, cout, device="cuda")
+        flops = 2.0 * B * H * W * cout * cin * 9
+        row = {"name": name}
+        for sp in (1,) + tuple(splits):
+            ops._splitk_count = (lambda *a, _s=sp, **k: _s)
+            try:
+                fn = lambda: ops.conv2d(x, p, emb=emb)  # noqa: E731
+                ms = timeit(fn)
+            finally:
+                ops._splitk_count = orig
+            row[f"s{sp}"] = round(flops / ms / 1e9, 1)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
