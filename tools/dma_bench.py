@@ -32,8 +32,13 @@ SHAPES = [
     ("lin320x320", 1, 65536, 1, 320, 0, 320, 1, 1, 0, None),
     ("lin1280x1280", 1, 4096, 1, 1280, 0, 1280, 1, 1, 0, None),
     ("tail3x20x20_128to192", 3, 20, 20, 128, 0, 192, 3, 1, 0, None),
+    ("comp5x5_256to128@32", 16, 32, 32, 256, 0, 128, 5, 1, 0, None),
+    ("comp5x5_128to128@32", 16, 32, 32, 128, 0, 128, 5, 1, 0, None),
+    ("comp3x3_256to384@32", 16, 32, 32, 256, 0, 384, 3, 1, 0, None),
+    ("unet_cat640+320@32_1x1", 16, 32, 32, 640, 320, 640, 1, 1, 0, None),
+    ("unet_cat1280+640@32_1x1", 16, 32, 32, 1280, 640, 640, 1, 1, 0, None),
 ]
-TILES = (-1, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35)
+TILES = (-1, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36)
 
 
 def bench(fn, reps):
