@@ -31,6 +31,10 @@ SHAPES = [
     ("lin320x2560", 1, 65536, 1, 320, 0, 2560, 1, 1, 0, None),
     ("lin320x320", 1, 65536, 1, 320, 0, 320, 1, 1, 0, None),
     ("lin1280x1280", 1, 4096, 1, 1280, 0, 1280, 1, 1, 0, None),
+    ("lin640x640", 1, 16384, 1, 640, 0, 640, 1, 1, 0, None),
+    ("lin1280x3840", 1, 4096, 1, 1280, 0, 3840, 1, 1, 0, None),
+    ("lin5120x1280", 1, 4096, 1, 5120, 0, 1280, 1, 1, 0, None),
+    ("lin2560x640", 1, 16384, 1, 2560, 0, 640, 1, 1, 0, None),
     ("tail3x20x20_128to192", 3, 20, 20, 128, 0, 192, 3, 1, 0, None),
     ("comp5x5_256to128@32", 16, 32, 32, 256, 0, 128, 5, 1, 0, None),
     ("comp5x5_128to128@32", 16, 32, 32, 128, 0, 128, 5, 1, 0, None),
