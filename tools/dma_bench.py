@@ -15,6 +15,7 @@ from rdeic_amd import ops  # noqa: E402
 # name, B, H, W, c0, c1, cout, k, stride, up2, pad_tl (None = k//2)
 SHAPES = [
     ("vae128@512", 16, 512, 512, 128, 0, 128, 3, 1, 0, None),
+    ("vae128@1024", 8, 1024, 1024, 128, 0, 128, 3, 1, 0, None),
     ("vae256@256", 16, 256, 256, 256, 0, 256, 3, 1, 0, None),
     ("vae512@128", 16, 128, 128, 512, 0, 512, 3, 1, 0, None),
     ("vae512@64", 16, 64, 64, 512, 0, 512, 3, 1, 0, None),
