@@ -245,6 +245,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const T* __restrict__ x, 
 // 256 % (c / 8) == 0 (every VAE / compressor width: 128, 256, 512) a thread's U chunks share one
 // channel group, so its 64 bytes of (a, b) are loaded once instead of U times (the per-chunk table
 // reads were 4x the x traffic through L1 / TA).
+constexpr int GN_APPLY_LDS_C = 2560;  // widest non-uniform GroupNorm input (the UNet's 2560-channel concat)
+
 template <bool UNIFORM, int U>
 __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const bf16* __restrict__ x, int n, int hw, int c, int ld,
                                                            const float* __restrict__ ab, int ab_c, int silu,
@@ -266,15 +268,23 @@ __global__ __launch_bounds__(256) void gn_apply_vec_kernel(const bf16* __restric
     if (i < total) v[u] = *reinterpret_cast<const bf16x8*>(xi + (long)pix[u] * ld + ch[u]);
   }
   float4 sab[4];
+  // non-uniform widths (the UNet's 320 ... 2560 channels): the image's (a, b) table goes to LDS once
+  // per block (<= 20 KB), behind the x loads already in flight, so the per-chunk table reads are
+  // LDS reads instead of 4x the x traffic through the vector cache
+  __shared__ __attribute__((aligned(16))) float lab[UNIFORM ? 4 : 2 * GN_APPLY_LDS_C];
   if (UNIFORM) {
     const float4* p = reinterpret_cast<const float4*>(abi + ch[0] * 2);
 #pragma unroll
     for (int q = 0; q < 4; ++q) sab[q] = p[q];
+  } else {
+    for (int i = threadIdx.x; i < cp * 4; i += 256)
+      reinterpret_cast<float4*>(lab)[i] = reinterpret_cast<const float4*>(abi)[i];
+    __syncthreads();
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (base + u * 256 >= total) break;
-    const float4* p = reinterpret_cast<const float4*>(abi + ch[u] * 2);
+    const float4* p = reinterpret_cast<const float4*>(lab + ch[u] * 2);
     bf16x8 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -563,7 +573,8 @@ extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32
   ProfScope ps(s, RDEIC_PROF_GN_APPLY, 2.0 * n * hw * c * (dtype == 1 ? 2 : 4));
   long total = (long)n * hw * c;
   if (dtype == 1 && c % 8 == 0 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
-      ((uintptr_t)y) % 16 == 0 && ((uintptr_t)ab) % 16 == 0) {
+      ((uintptr_t)y) % 16 == 0 && ((uintptr_t)ab) % 16 == 0 && (ab_c % 2) == 0 &&
+      (256 % (c / 8) == 0 || c <= GN_APPLY_LDS_C)) {
     if ((long)hw * (c / 8) >= (1L << 31) - 2048) return RDEIC_EINVAL;
     if (256 % (c / 8) == 0) {
       const int blocks = (int)(((long)hw * (c / 8) + 2047) / 2048);
