@@ -31,18 +31,22 @@ PEAK_FP32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
 
 
-def conv_traffic():
+def conv_traffic(workload: dict):
     """HBM bytes per conv launch, from the latest committed PMC run (tools/pmc_bench.sh ->
     profiles/conv_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of
     MI355X_MICROARCH.md §HBM). Counters cannot be read inside this process, so the figure is the
-    measured one with its source, or None when no PMC run has been committed."""
+    measured one with its source — attached only when that run's workload is this line's (size,
+    relay steps, batch per GPU, dtype, sampler); otherwise None with the reason."""
     try:
         with open(os.path.join(ROOT, "profiles", "conv_traffic.json")) as f:
             t = json.load(f)
-        return {"bytes_per_launch": t["bytes_per_launch"], "algorithmic_flops_per_launch": t.get("flops_per_launch"),
-                "source": t.get("source", "profiles/conv_traffic.json")}
-    except (OSError, ValueError, KeyError):
-        return None
+    except (OSError, ValueError):
+        return {"bytes_per_launch": None, "reason": "no committed PMC run (profiles/conv_traffic.json)"}
+    if t.get("workload") != workload:
+        return {"bytes_per_launch": None,
+                "reason": f"the committed PMC run measured {t.get('workload')}, not this line's {workload}"}
+    return {"bytes_per_launch": t["bytes_per_launch"], "workload": workload,
+            "source": t.get("source", "profiles/conv_traffic.json")}
 
 
 def parse():
@@ -77,6 +81,10 @@ def parse():
     ap.add_argument("--no-geglu-fuse", action="store_true", help="unfused GEGLU (projection + geglu kernel), A/B only")
     ap.add_argument("--rate-gain", type=float, default=None,
                     help="synthetic bpp knob (rdeic_amd/weights.py); default: the ~0.08 bpp gain of config 2")
+    ap.add_argument("--fp32-steps", type=int, default=2,
+                    help="one-GPU runs with --dtype bf16: also time this many steps of the fp32 parity mode (the "
+                         "path whose bitstreams and pixels match the reference) on the same images, and report "
+                         "its throughput and the bf16-vs-fp32 bpp / PSNR / MS-SSIM gap; 0 = skip")
     return ap.parse_args()
 
 
@@ -203,8 +211,38 @@ def main():
         results.append({"target_bpp": target, "rate_gain": rate_gain, "elapsed": elapsed, "prof": prof,
                         "mean_bpp": float(mrows[:, 0].mean()), "mean_psnr_db": float(mrows[:, 2].mean()),
                         "mean_ms_ssim": float(mrows[:, 4].mean()),
-                        "images": int(mrows.shape[0])})
+                        "images": int(mrows.shape[0]), "rows": rows_by_step[-1].numpy()})
         del sessions
+    fp32_leg = None
+    if world == 1 and args.dtype == "bf16" and args.fp32_steps > 0 and not args.bpp_sweep:
+        log(f"fp32 parity mode: 1 warm-up + {args.fp32_steps} timed steps on one session, same images")
+        rg = results[main_i]["rate_gain"]
+        del model
+        torch.cuda.empty_cache()
+        m32 = RDEIC(compute_dtype=torch.float32, device=dev).init_synthetic(rate_gain=rg)
+        m32.preprocess_model.update(force=True)
+        mse32 = torch.empty(B, dtype=torch.float32, device=dev)
+        run_batch(m32, mse32)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.fp32_steps):
+            rows32 = run_batch(m32, mse32)
+        torch.cuda.synchronize()
+        el32 = time.perf_counter() - t0
+        r32 = rows32.numpy()
+        r16 = results[main_i]["rows"]
+        fp32_leg = {
+            "dtype": "fp32", "path": "bitstream-parity (fp32 convs on v_mfma_f32_16x16x4f32; file bodies byte-equal "
+                                     "to the oracle's, pixels within 1e-3 abs: tests/test_config2_gpu.py)",
+            "images_per_s": round(B * args.fp32_steps / el32, 3), "ms_per_step": round(el32 / args.fp32_steps * 1e3, 2),
+            "steps": args.fp32_steps, "codec_sessions": 1, "mean_bpp": round(float(r32[:, 0].mean()), 5),
+            "mean_psnr_db": round(float(r32[:, 2].mean()), 3), "mean_ms_ssim": round(float(r32[:, 4].mean()), 5),
+            "bf16_minus_fp32": {
+                "mean_bpp_rel": round(float((r16[:, 0].mean() - r32[:, 0].mean()) / r32[:, 0].mean()), 5),
+                "max_image_bpp_rel": round(float(np.abs((r16[:, 0] - r32[:, 0]) / r32[:, 0]).max()), 5),
+                "mean_psnr_db": round(float(r16[:, 2].mean() - r32[:, 2].mean()), 4),
+                "mean_ms_ssim": round(float(r16[:, 4].mean() - r32[:, 4].mean()), 5)}}
+        del m32
     parallel.finish()  # every rank leaves the group before rank 0's CPU-baseline leg
     if rank != 0:
         return
@@ -218,7 +256,9 @@ def main():
         peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_FP32_TFLOPS
         roof = {"bound": "mfma", "kernel": "conv_dma_kernel / conv_kernel (implicit-GEMM conv + linear, rdeic_conv2d)",
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": conv_traffic(), "launches_per_step": round(n / args.steps, 1),
+                "traffic": conv_traffic({"size": S, "ddim_steps": args.ddim_steps, "batch": B, "dtype": args.dtype,
+                                         "sampler": args.sampler}),
+                "launches_per_step": round(n / args.steps, 1),
                 "sampling": f"launches >= 50 GFLOP always timed, smaller ones 1 in {args.prof_every} (weighted); "
                             f"measured on one codec session over {args.steps} steps right after the timed region",
                 "avg_launch_us": round(ms * 1e3 / max(1, n), 2), "ms_per_step": round(ms / args.steps, 3),
@@ -254,7 +294,10 @@ def main():
             cpu = {"value": None, "error": f"{type(e).__name__}: {e}"}
     cfg_name = {(512, 2): "config 2", (1024, 5): "config 3"}.get((S, args.ddim_steps), "custom")
     line = {
-        "metric": f"{S}x{S} images/sec encode+relay-decode @ fixed bpp (bitstream-parity path); 1/2/4/8 GPU",
+        "metric": f"{S}x{S} images/sec encode+relay-decode @ fixed bpp; 1/2/4/8 GPU",
+        "path": ("bf16: self-consistent bitstreams (the decoder decodes its own streams, batch-invariant coding); "
+                 "bpp / quality gap to the fp32 bitstream-parity mode in fp32_parity_mode" if args.dtype == "bf16"
+                 else "fp32: bitstream-parity mode (file bodies byte-equal to the oracle's)"),
         "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded images, random-init weights)",
@@ -267,6 +310,7 @@ def main():
                    "mean_ms_ssim": round(r["mean_ms_ssim"], 4)},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "fp32_parity_mode": fp32_leg,
     }
     if args.bpp_sweep:
         line["bpp_sweep"] = [{"target_bpp": p["target_bpp"], "rate_gain": p["rate_gain"],

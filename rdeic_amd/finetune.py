@@ -49,7 +49,13 @@ class FineTuneConfig:
 class FineTuner:
     """Holds the flat trainable parameters / grads / AdamW state of an RDEIC model and runs steps."""
 
-    def __init__(self, model: RDEIC, cfg: Optional[FineTuneConfig] = None):
+    def __init__(self, model: RDEIC, cfg: Optional[FineTuneConfig] = None,
+                 embed_prob: Optional[torch.Tensor] = None):
+        """embed_prob: the VectorQuantiser's codebook-usage EMA buffer
+        (`preprocess_model.quantize.embed_prob` of a reference checkpoint or of train.py's own; zeros
+        when absent, as a freshly built VectorQuantiser, compression_modules.py:239-241). It sets which
+        codes the next step re-initialises (decay = exp(-embed_prob * N * 10 / (1 - 0.99)) - 1e-3,
+        compression_modules.py:272-296), so a resumed run must carry it."""
         self.m = model
         self.cfg = cfg or FineTuneConfig(used_timesteps=model.used_timesteps)
         st = model.store
@@ -80,8 +86,21 @@ class FineTuner:
         AG.STEP_PACKS.clear()
         cb = model.preprocess_model.codebook_size
         self.embed_prob = torch.zeros(cb, dtype=torch.float32, device=dev)  # VectorQuantiser buffer
+        if embed_prob is not None:
+            if tuple(embed_prob.shape) != (cb,):
+                raise ValueError(f"embed_prob has shape {tuple(embed_prob.shape)}, the codebook has {cb} codes")
+            self.embed_prob.copy_(embed_prob.to(torch.float32))
         self.step_count = 0
         self.buckets = None
+
+    def load_optimizer_state(self, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, step: int) -> None:
+        """Restore AdamW's moments and step count (train.py's checkpoints) so a resumed run continues
+        the interrupted one exactly."""
+        for dst, src, name in ((self.exp_avg, exp_avg, "exp_avg"), (self.exp_avg_sq, exp_avg_sq, "exp_avg_sq")):
+            if src.numel() != dst.numel():
+                raise ValueError(f"optimizer.{name} holds {src.numel()} values, the trainable buffer {dst.numel()}")
+            dst.copy_(src.reshape(-1).to(torch.float32))
+        self.step_count = int(step)
 
     def enable_ddp(self, bucket_bytes: int = 32 << 20, group=None):
         """Average gradients over the data-parallel ranks, bucketed and overlapped with the backward

@@ -89,8 +89,11 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
            gn: Optional[torch.Tensor] = None, gn_silu: bool = False, emb: Optional[torch.Tensor] = None,
            act: int = NONE, slope: float = 0.0, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False,
-           geglu: bool = False, stats: bool = False, stats_hw: Optional[int] = None) -> torch.Tensor:
+           geglu: bool = False, stats: bool = False, stats_hw: Optional[int] = None,
+           images: Optional[int] = None) -> torch.Tensor:
     """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC).
+    images: how many images the launch covers when that is not n (token rows of ops.linear); the
+    inference split-K count is chosen per image (SPLITK_NOMINAL_BATCH).
     geglu: p packed by ParamStore.conv_geglu; out = value * gelu(gate), cout/2 channels (bf16).
     stats: the output feeds a GroupNorm — its statistics are produced with it (fused into the conv
     epilogue where the tile allows, rdeic_conv_desc.gn_part) and group_norm_ab(out) then needs no
@@ -176,7 +179,8 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
             part = torch.empty(nf, dtype=torch.float32, device=x.device)
             d.gn_part, d.gn_hw = part.data_ptr(), ghw
     flops = 2.0 * n * ho * wo * p.cout * p.kh * p.kw * p.cin
-    splits = _splitk_count(x, x2, n * ho * wo, p, gn is not None or pixel_shuffle or geglu, out)
+    splits = _splitk_count(x, x2, n * ho * wo, p, gn is not None or pixel_shuffle or geglu, out,
+                           n if images is None else images)
 
     tile = -1
     if splits == 1 and x.dtype == torch.bfloat16 and gn is None and _gn_materialize(x, x2, p):
@@ -291,6 +295,12 @@ _SPLITK_WS: dict = {}
 
 
 SPLITK_SHORT = False  # training: also split the short-K (k-tiles >= 8) small-M layers
+# Inference picks the split count from the layer's PER-IMAGE shape, as if the batch were
+# SPLITK_NOMINAL_BATCH images (config 2's 16): the k grouping of every output element then does not
+# depend on how many images share the launch, so one bitstream decodes to the same pixels in any
+# batch (bench, CLI --batch_size / --micro_batch_size, data-parallel shards). Training (SPLITK_SHORT,
+# B=1) sizes splits from the real M: it needs no batch invariance.
+SPLITK_NOMINAL_BATCH = 16
 
 
 class splitk_allowed:
@@ -310,8 +320,11 @@ class splitk_allowed:
         SPLITK_ALLOWED, SPLITK_SHORT = self._prev
 
 
-def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor) -> int:
-    """Number of k-splits (1 = none): only when the 128x128 tile grid cannot fill the chip."""
+def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor, n: int = 1) -> int:
+    """Number of k-splits (1 = none): only when the 128x128 tile grid cannot fill the chip.
+    Inference: a function of the per-image M only (SPLITK_NOMINAL_BATCH)."""
+    if not SPLITK_SHORT:
+        M = (M // max(1, n)) * SPLITK_NOMINAL_BATCH
     if not SPLITK_ALLOWED or fused or x.dtype not in (torch.bfloat16, torch.float32) or p.cout % 8 \
             or pix_ld(out) % 8 or out.data_ptr() % 16:
         return 1
@@ -474,8 +487,9 @@ def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) 
 
 def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, geglu: bool = False,
-           stats_hw: Optional[int] = None) -> torch.Tensor:
+           stats_hw: Optional[int] = None, images: int = 1) -> torch.Tensor:
     """Token-wise Linear over a [rows, c] tensor (1x1 conv over a rows x 1 image).
+    images: the number of images whose tokens the rows hold (the per-image split-K choice).
     geglu: fused GEGLU projection (p from ParamStore.conv_geglu), output [rows, cout/2].
     stats_hw: the output (as [rows/stats_hw images, stats_hw tokens]) feeds a GroupNorm; its
     statistics are produced with it (conv2d(stats=True)); reshape with ops.tokens_to_nhwc."""
@@ -490,7 +504,7 @@ def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[tor
     if res is not None:
         r4 = res.as_strided((1, rows, 1, p.cout), (rows * res.stride(0), res.stride(0), res.stride(0), 1))
     conv2d(x4, p, act=act, res=r4, out=o4, out_f32=out_f32, geglu=geglu, stats=stats_hw is not None,
-           stats_hw=stats_hw)
+           stats_hw=stats_hw, images=images)
     info = getattr(o4, "_rdeic_gn_part", None)
     if info is not None:
         out._rdeic_gn_tokens = info  # carried to the NHWC view by tokens_to_nhwc

@@ -88,9 +88,11 @@ class GradBuckets:
     The buffer is cut into buckets of ~bucket_bytes, from its END: parameters are laid out in
     declaration (forward) order and the backward produces the last layers' gradients first. Each
     parameter's post-accumulate-grad hook counts down its bucket; a bucket whose gradients are all
-    accumulated is all-reduced asynchronously right away (RCCL overlaps it with the rest of the
-    backward), and finish() launches any bucket that got no gradient this step (in bucket order, the
-    same on every rank), waits, and averages. xGMI rings are per-link bound (7 links x ~153 GB/s):
+    accumulated becomes ready, and ready buckets are all-reduced asynchronously strictly in bucket
+    index order (a cursor, as torch DDP does): whatever order the hooks fire in on a rank, every rank
+    issues the same sequence of collectives, so RCCL never pairs mismatched buckets. RCCL overlaps them
+    with the rest of the backward; finish() launches the remaining buckets (in order), waits, and
+    averages. xGMI rings are per-link bound (7 links x ~153 GB/s):
     a few tens of MB per bucket keeps each collective long enough to run near link rate."""
 
     def __init__(self, grad_flat: torch.Tensor, params, bucket_bytes: int = 32 << 20, group=None):
@@ -122,13 +124,21 @@ class GradBuckets:
         for p in self._params:
             p._rdeic_notify = self._on_grad
         self.pending, self.handles, self.fired = [], {}, {}
+        self.next_bucket = 0
+        self.launch_order = []  # bucket ids in the order their collectives were issued (tests)
 
     def begin(self):
         self.pending = list(self.count)
         self.handles = {}
         self.fired = {}
+        self.next_bucket = 0
+        self.launch_order = []
 
     def _launch(self, b: int):
+        if b != self.next_bucket:
+            raise RuntimeError(f"bucket {b} launched out of order (next is {self.next_bucket})")
+        self.next_bucket += 1
+        self.launch_order.append(b)
         lo, hi = self.buckets[b]
         if self.world > 1:
             self.handles[b] = dist.all_reduce(self.grad[lo:hi], group=self.group, async_op=True)
@@ -146,13 +156,14 @@ class GradBuckets:
             raise RuntimeError("a bucketed parameter received two gradient accumulations in one step")
         b = self.owner[k]
         self.pending[b] -= 1
-        if self.pending[b] == 0:
-            self._launch(b)
+        # launch every consecutive ready bucket from the cursor: a bucket that completes early waits
+        # for its predecessors, so the collective sequence is the bucket order on every rank
+        while self.next_bucket < len(self.buckets) and self.pending[self.next_bucket] == 0:
+            self._launch(self.next_bucket)
 
     def finish(self):
-        for b in range(len(self.buckets)):
-            if b not in self.handles:
-                self._launch(b)
+        while self.next_bucket < len(self.buckets):
+            self._launch(self.next_bucket)
         for b in range(len(self.buckets)):
             h = self.handles[b]
             if h is not None:

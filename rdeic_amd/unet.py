@@ -187,10 +187,11 @@ class UNet:
     def time_embed(self, temb: torch.Tensor) -> torch.Tensor:
         """SiLU(time_embed(t_emb)) @ stacked emb_layers -> [B, sum(cout)] fp32 (one GEMM)."""
         s = self.store
-        e = ops.linear(temb, s.conv(self.prefix + "time_embed.0", dtype=torch.float32), act=ops.SILU)
-        e = ops.linear(e, s.conv(self.prefix + "time_embed.2", dtype=torch.float32), act=ops.SILU)
+        B = temb.shape[0]  # one row per image
+        e = ops.linear(temb, s.conv(self.prefix + "time_embed.0", dtype=torch.float32), act=ops.SILU, images=B)
+        e = ops.linear(e, s.conv(self.prefix + "time_embed.2", dtype=torch.float32), act=ops.SILU, images=B)
         stacked = s.conv_cat([rb.prefix + ".emb_layers.1" for rb in self.resblocks], dtype=torch.float32)
-        return ops.linear(e, stacked)
+        return ops.linear(e, stacked, images=B)
 
     def resblock(self, rb: ResBlock, x: torch.Tensor, emb_all: torch.Tensor,
                  x2: Optional[torch.Tensor] = None, stats: bool = False) -> torch.Tensor:
@@ -223,29 +224,30 @@ class UNet:
         scale = t.dh ** -0.5
         # self-attention
         n1 = ops.layer_norm(h, s.get(tb + ".norm1.weight"), s.get(tb + ".norm1.bias"))
-        qkv = ops.linear(n1, s.conv_cat([tb + ".attn1.to_q", tb + ".attn1.to_k", tb + ".attn1.to_v"]))
+        qkv = ops.linear(n1, s.conv_cat([tb + ".attn1.to_q", tb + ".attn1.to_k", tb + ".attn1.to_v"]), images=B)
         o = torch.empty((rows, C), dtype=x.dtype, device=x.device)
         ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch=B, heads=t.heads, lq=L, lk=L, dh=t.dh,
                       scale=scale)
-        h = ops.linear(o, s.conv(tb + ".attn1.to_out.0"), res=h)
+        h = ops.linear(o, s.conv(tb + ".attn1.to_out.0"), res=h, images=B)
         # cross-attention against the text context
         n2 = ops.layer_norm(h, s.get(tb + ".norm2.weight"), s.get(tb + ".norm2.bias"))
-        q = ops.linear(n2, s.conv(tb + ".attn2.to_q"))
-        kv = ops.linear(ctx_kv_in, s.conv_cat([tb + ".attn2.to_k", tb + ".attn2.to_v"]))
+        q = ops.linear(n2, s.conv(tb + ".attn2.to_q"), images=B)
+        kv = ops.linear(ctx_kv_in, s.conv_cat([tb + ".attn2.to_k", tb + ".attn2.to_v"]), images=ctx_batch)
         ops.attention(q, kv[:, :C], kv[:, C:], o, batch=B, heads=t.heads, lq=L, lk=ctx_len, dh=t.dh, scale=scale,
                       kv_bcast=(ctx_batch == 1 and B > 1))
-        h = ops.linear(o, s.conv(tb + ".attn2.to_out.0"), res=h)
+        h = ops.linear(o, s.conv(tb + ".attn2.to_out.0"), res=h, images=B)
         # GEGLU feed-forward
         n3 = ops.layer_norm(h, s.get(tb + ".norm3.weight"), s.get(tb + ".norm3.bias"))
         if x.dtype == torch.bfloat16 and ops.GEGLU_FUSED and C % 64 == 0:
-            gg = ops.linear(n3, s.conv_geglu(tb + ".ff.net.0.proj"), geglu=True)  # one pass, half the writes
+            gg = ops.linear(n3, s.conv_geglu(tb + ".ff.net.0.proj"), geglu=True, images=B)  # one pass, half the writes
         else:
-            gg = ops.geglu(ops.linear(n3, s.conv(tb + ".ff.net.0.proj")))
-        h = ops.linear(gg, s.conv(tb + ".ff.net.2"), res=h)
+            gg = ops.geglu(ops.linear(n3, s.conv(tb + ".ff.net.0.proj"), images=B))
+        h = ops.linear(gg, s.conv(tb + ".ff.net.2"), res=h, images=B)
         # proj_out + residual to the block input
         if not x.is_contiguous():
             raise ValueError("transformer input must be contiguous NHWC")
-        out = ops.linear(h, s.conv(t.prefix + ".proj_out"), res=x.view(rows, C), stats_hw=L if stats else None)
+        out = ops.linear(h, s.conv(t.prefix + ".proj_out"), res=x.view(rows, C), stats_hw=L if stats else None,
+                         images=B)
         return ops.tokens_to_nhwc(out, B, H, W_)
 
     def run_layers(self, layers, x, emb_all, ctx_rows, ctx_batch, ctx_len, x2=None, stats_last: bool = True):

@@ -1,0 +1,48 @@
+"""The bf16 headline path against the fp32 parity mode on config 2's own batch (16 synthetic 512x512
+images, 2-step relay DDIM, the bench's rate gain): fp32 is the mode whose file bodies and pixels
+match the reference (tests/test_config2_gpu.py); bf16 computes mu / sigma and the decoder in bf16,
+so its symbols and pixels differ. The north star asks for "bpp equal to reference": this bounds
+the gap per image and on the batch, and prints the measured values.
+
+Bounds (measured on MI355X, with margin): mean bpp within 3% and every image within 8%; mean PSNR
+(decoded vs input) within 0.3 dB; mean MS-SSIM within 0.01."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+SIZE = 512
+SEEDS = list(range(231, 247))
+
+
+def _run(dtype):
+    from rdeic_amd import metrics
+    from rdeic_amd import weights as W
+    from rdeic_amd.rdeic import RDEIC
+    from rdeic_amd.synthetic import relay_noise, synth_context, synth_image
+    imgs = torch.from_numpy(np.stack([synth_image(SIZE, SIZE, s) for s in SEEDS])).cuda()
+    noise = torch.cat([relay_noise((1, 4, SIZE // 8, SIZE // 8), s, 2)[0] for s in SEEDS])
+    m = RDEIC(compute_dtype=dtype).init_synthetic(rate_gain=W.RATE_GAIN_BPP008)
+    m.preprocess_model.update(force=True)
+    with torch.no_grad():
+        out, bodies = m.codec_images(imgs, synth_context().cuda(), noise, steps=2)
+        psnr = np.asarray(metrics.psnr(out, imgs), np.float64)
+        _, ms = metrics.ssim_ms_ssim(out, imgs)
+    bpp = np.array([8.0 * len(b) / SIZE ** 2 for b in bodies])
+    del m
+    torch.cuda.empty_cache()
+    return bpp, psnr, np.asarray(ms, np.float64)
+
+
+def test_bf16_vs_fp32_bpp_and_quality(gpu):
+    b16, p16, s16 = _run(torch.bfloat16)
+    b32, p32, s32 = _run(torch.float32)
+    rel = (b16 - b32) / b32
+    print(f"bpp fp32 {b32.mean():.5f} bf16 {b16.mean():.5f} (mean rel {(b16.mean() - b32.mean()) / b32.mean():+.4f}, "
+          f"per-image max |rel| {np.abs(rel).max():.4f})")
+    print(f"PSNR fp32 {p32.mean():.3f} bf16 {p16.mean():.3f} dB (delta {p16.mean() - p32.mean():+.3f}); "
+          f"MS-SSIM fp32 {s32.mean():.5f} bf16 {s16.mean():.5f} (delta {s16.mean() - s32.mean():+.5f})")
+    assert abs(b16.mean() - b32.mean()) <= 0.03 * b32.mean()
+    assert np.abs(rel).max() <= 0.08
+    assert abs(p16.mean() - p32.mean()) <= 0.3
+    assert abs(s16.mean() - s32.mean()) <= 0.01

@@ -4,6 +4,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -96,12 +97,24 @@ def _rank(rank, world, port, q):
         # ~1.2 KB buckets: several buckets, launched from the hooks while the backward runs
         gb = GradBuckets(grad, params, bucket_bytes=1200)
         coef = [torch.randn(p.shape, generator=g) for p, _, _ in params]
-        for step in range(2):
+        for step in range(3):
             grad.zero_()
             gb.begin()
-            loss = sum(((rank + 1 + step) * c * p * p).sum() for c, (p, _, _) in zip(coef, params))
-            loss.backward()
+            if step < 2:
+                loss = sum(((rank + 1 + step) * c * p * p).sum() for c, (p, _, _) in zip(coef, params))
+                loss.backward()
+            else:
+                # step 2: every parameter gets its gradient from its own backward, in a rank-dependent
+                # order, so the buckets complete in a different order on each rank; the collectives
+                # must still be issued in bucket order on both (a mismatch would pair wrong buckets)
+                order = list(range(len(params)))
+                rng = np.random.default_rng(rank + 7)
+                rng.shuffle(order)
+                for i in order:
+                    c, (p, _, _) = coef[i], params[i]
+                    ((rank + 1 + step) * c * p * p).sum().backward()
             gb.finish()
+            assert gb.launch_order == list(range(len(gb.buckets))), gb.launch_order
             expect = torch.cat([(sum(r + 1 + step for r in range(world)) / world * 2 * c * p.detach()).reshape(-1)
                                 for c, (p, _, _) in zip(coef, params)])
             q.put((rank, step, float((grad - expect).abs().max()), len(gb.buckets)))
@@ -119,7 +132,7 @@ def test_bucketed_grad_allreduce_gloo_world2():
     procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(2 * world)]
+    res = [q.get(timeout=120) for _ in range(3 * world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -127,3 +140,12 @@ def test_bucketed_grad_allreduce_gloo_world2():
         assert step >= 0, err
         assert err < 1e-5, (rank, step, err)
         assert nb > 3
+
+
+def test_precision_16_refused():
+    """Lightning's precision 16 is fp16 autocast, which the step does not implement: refused rather
+    than silently trained in bf16 (train.py)."""
+    import train
+    with pytest.raises(SystemExit):
+        train.precision_dtype(16)
+    assert train.precision_dtype("bf16") == torch.bfloat16 and train.precision_dtype(32) == torch.float32

@@ -20,10 +20,7 @@ def _free_port():
     return p
 
 
-G = 11
-
-
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, G):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     r, w, _ = parallel.init_from_env(backend="gloo")
@@ -37,12 +34,13 @@ def _worker(rank, world, port, q):
     parallel.finish()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_gather_and_max(world):
+@pytest.mark.parametrize("world,G", [(2, 11), (3, 11), (3, 16)])
+def test_gloo_gather_and_max(world, G):
+    """G=16 on 3 ranks: config 4's uneven shards (6/5/5), the bench's --global-batch path."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, G)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -32,7 +32,8 @@ def test_single_head_attention_chunked_is_exact(gpu, dtype):
     torch.testing.assert_close(full.float().view(B, L, C), ref, rtol=tol, atol=tol)
 
 
-@pytest.mark.parametrize("B,L,spread", [(2, 1024, 1.0), (1, 4096, 1.0), (2, 256, 6.0), (1, 96, 1.0)])
+@pytest.mark.parametrize("B,L,spread", [(2, 1024, 1.0), (1, 4096, 1.0), (2, 256, 6.0), (1, 96, 1.0),
+                                        (1, 16384, 1.0)])  # 16384: config 3's 1024^2 mid-block
 def test_flash_d512_matches_fp32_reference(gpu, B, L, spread):
     """The flash kernel (rdeic_attention, dh = 512, bf16): no score buffer; against torch fp32 on the
     same bf16 inputs, on the AttnBlock's [B*L, 3C] qkv layout (row stride 3C). spread > 1 gives
@@ -52,7 +53,7 @@ def test_flash_d512_matches_fp32_reference(gpu, B, L, spread):
     # bf16 probabilities (P) and bf16 output: ~1e-2 relative to the output scale
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max().item()
     assert err.mean().item() < 2e-3 * max(1.0, ref.abs().max().item()), err.mean().item()
-    if spread == 1.0 and L % 64 == 0:
+    if spread == 1.0 and L % 64 == 0 and L <= 4096:
         mat = torch.empty_like(out)
         ops.attention_single_head_materialized(q, k, v, mat, batch=B, length=L, dim=C, scale=scale)
         assert (mat.float() - out.float()).abs().max().item() < 2e-2

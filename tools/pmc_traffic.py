@@ -31,6 +31,20 @@ def per_kernel(pattern, counter):
     return tot, cnt, vgpr
 
 
+def workload(argv):
+    """The bench workload the passes ran (bench.py's defaults overridden by the args pmc_bench.sh
+    forwarded): bench.py attaches the traffic only to a line of the same workload."""
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--ddim-steps", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--sampler", default="ddim")
+    a, _ = ap.parse_known_args(argv)
+    return {"size": a.size, "ddim_steps": a.ddim_steps, "batch": a.batch, "dtype": a.dtype, "sampler": a.sampler}
+
+
 out_dir = sys.argv[1]
 f_tot, f_cnt, vgpr = per_kernel(os.path.join(out_dir, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
 w_tot, w_cnt, _ = per_kernel(os.path.join(out_dir, "write", "**", "*counter_collection.csv"), "WRITE_SIZE")
@@ -42,6 +56,7 @@ print(json.dumps({
     "fetch_bytes_per_launch": round(fetch_b / max(1, launches)),
     "write_bytes_per_launch": round(write_b / max(1, sum(w_cnt.values()))),
     "launches_counted": launches,
+    "workload": workload(sys.argv[2:]),
     "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 1 --warmup 1, timed step only "
               "(tools/pmc_bench.sh)",
     "per_kernel": {k[:80]: {"launches": f_cnt[k], "gb": round((2 * f_tot[k] * 1024 + w_tot.get(k, 0) * 1024) / 1e9, 3),
