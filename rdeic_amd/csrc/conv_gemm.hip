@@ -1100,7 +1100,8 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
 // Measured (tools/dma_bench.py, one MI355X): 32 is best where a 256x256 grid fills the chip
 // without padding waste (1.19-1.27 PF on the VAE 512-channel layers), 25 on the rest with >= 256
 // 128x128 tiles, the 4-wave 64x128 tile when even that grid cannot fill the chip; 34 often wins
-// on short-K linears (the autotuner in rdeic_amd/ops.py picks per shape).
+// on short-K linears (the committed per-shape table rdeic_amd/conv_tiles.json picks, measured by
+// tools/tune_tiles.py; shapes missing from it use this heuristic).
 int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int tile,
                     int gn_hw = 0, bool* fused = nullptr) {
   if (tile < 20 || tile > 36) {

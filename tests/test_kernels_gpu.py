@@ -276,7 +276,7 @@ def test_conv_splitk(gpu, cin, cout, hw, res):
     p = ops.ConvParams.pack(w, b, pad=1, dtype=torch.bfloat16)
     xd, rd = _nhwc(x.to(torch.bfloat16)), _nhwc(r.to(torch.bfloat16))
     with ops.splitk_allowed():
-        assert ops._splitk_count(xd, None, B * hw * hw, p, False, rd) > 1
+        assert ops._splitk_count(xd, None, B * hw * hw, p, False, rd, B) > 1
         out = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
     torch.testing.assert_close(_nchw(out), ref, rtol=2e-2, atol=3e-2)
     out_plain = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
@@ -300,8 +300,8 @@ def test_conv_splitk_fp32(gpu, cin, cout, hw, k, res):
         ref = ref + r
     p = ops.ConvParams.pack(w, b, pad=k // 2, dtype=torch.float32)
     xd, rd = _nhwc(x), _nhwc(r)
-    with ops.splitk_allowed():
-        assert ops._splitk_count(xd, None, hw * hw, p, False, rd) > 1
+    with ops.splitk_allowed(short_k=True):  # training: split counts from the real M (B=1)
+        assert ops._splitk_count(xd, None, hw * hw, p, False, rd, 1) > 1
         out = ops.conv2d(xd, p, emb=emb.cuda(), act=ops.SILU, res=rd if res else None)
     assert out.dtype == torch.float32
     torch.testing.assert_close(_nchw(out), ref, rtol=1e-4, atol=1e-4)
