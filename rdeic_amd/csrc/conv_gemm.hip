@@ -120,9 +120,18 @@ __host__ __device__ __forceinline__ bool epi_vec_ok(const ConvArgs& a) {
          (!a.res || ((a.res_ld % 8) == 0 && ((uintptr_t)a.res % 16) == 0));
 }
 
-template <int BM, int BN, int WGM, int WGN, int NT, int P = 2>
+// Tile row -> output row (GEMM m) of the vector epilogue: the GEMM kernels' tiles are BM consecutive
+// rows from m0; the halo conv's tiles are image blocks whose 64-row wave rows are each contiguous.
+struct RowsFrom {
+  int m0;
+  __device__ __forceinline__ int operator()(int r) const { return m0 + r; }
+};
+
+template <int BM, int BN, int WGM, int WGN, int NT, int P = 2, class RowMap = RowsFrom>
 __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16], const ConvArgs& a,
-                                             int m0, int n0, int wm, int wn, int lane, int tid, char* lds) {
+                                             int m0, int n0, int wm, int wn, int lane, int tid, char* lds,
+                                             RowMap rmap = RowMap{0}) {
+  if constexpr (__is_same(RowMap, RowsFrom)) rmap.m0 = m0;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int HM = TM / P;                    // fragment rows per pass
@@ -160,7 +169,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
       const int pr = c / CPR, cc = c - pr * CPR;
       // pass-local row pr -> wave row block wm' = pr / (WTM/P), row within = pr % (WTM/P)
       const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
-      const int m = m0 + wmr * WTM + p * (WTM / P) + wr;
+      const int m = rmap(wmr * WTM + p * (WTM / P) + wr);
       const int nn = n0 + cc * 8;
       if (m >= a.M || nn >= a.cout) continue;
       float v[8];
@@ -238,7 +247,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
             for (int k = 0; k < (WTM / P) / 16; ++k) {
               const int off = w * WTM + p * (WTM / P) + k * 16;  // row offset inside the 64-row block
               const float* col = L + (wmr * (WTM / P) + k * 16) * SDW + j;
-              const int nv = a.M - (m0 + b * 64 + off);  // valid rows of this 16-row group
+              const int nv = a.M - (rmap(b * 64) + off);  // valid rows of this 16-row group
               float s1 = 0.f, s2 = 0.f;
               if (nv >= 16) {  // all 16 loads issued before the (row-ordered) sums
                 float y[16];
@@ -261,12 +270,12 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
     if (st) {
       const int b = tid / BN, j = tid - (tid / BN) * BN;
       const int nn = n0 + j;
-      if (b < BM / 64 && nn < a.cout && m0 + b * 64 < a.M) {  // blocks past M are not in the buffer
-        float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0) / 64 + b) * a.cout + nn) * 2;
+      if (b < BM / 64 && nn < a.cout && rmap(b * 64) < a.M) {  // blocks past M are not in the buffer
+        float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + rmap(b * 64)) / 64) * a.cout + nn) * 2;
         pp[0] = ((sg[0] + sg[1]) + sg[2]) + sg[3];
         pp[1] = ((qg[0] + qg[1]) + qg[2]) + qg[3];
       }
-      if (tid == 0 && m0 == 0 && n0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
+      if (tid == 0 && rmap(0) == 0 && n0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
     }
   }
 }
@@ -1179,6 +1188,228 @@ int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipSt
   return RDEIC_OK;  // *fused false if any group could not fuse: the caller recomputes the statistics
 }
 
+// ============================================================================================
+// 3x3 / stride-1 / pad-1 conv on a halo strip, with the input GroupNorm affine (+ SiLU) applied
+// ONCE per element in LDS: the VAE ResnetBlock's norm -> nonlinearity -> conv
+// (ldm/modules/diffusionmodules/model.py:131-151, Normalize + nonlinearity + conv1 / conv2).
+//
+// The im2col path (conv_dma_kernel) re-stages every input element for each of the 9 taps, so a
+// GroupNorm + SiLU fused into its staging costs 9x the VALU of the element-wise pass and loses to
+// materialising silu(a x + b) in HBM (one read + one write of the activation). Here a tile is an
+// image block of TR x TC = 4 x 64 output pixels x 128 output channels; per 32-channel block the
+// (TR + 2) x (TC + 2) halo of the RAW input is DMA'd to LDS once (buffer_load ... lds, 25 x 1 KB
+// pieces, zeros outside the image from the descriptor's range check), transformed in place
+// (x * a + b, then x * rcp(1 + e^-x): exactly the bf16 values rdeic_groupnorm_apply writes; halo
+// pixels outside the image stay zero = the conv's zero padding of the normalised tensor) and then
+// read by all 9 taps. The 32-channel weight slice of each tap streams through a 3-deep ring.
+// Per step (tap) a wave (one output row, 64 channels) issues 16 v_mfma_f32_16x16x32_bf16.
+// LDS 78 KB -> two blocks per CU, so one block's epilogue overlaps the other's main loop.
+// Swizzle: 16-byte chunk q of halo pixel / weight row s lives at slot q ^ (((s >> 2) & 1) << 1),
+// conflict-free for every ds_read_b128 lane group at any pixel offset (tap shift).
+// k order: 32-channel block major, tap minor — fixed per shape (deterministic, batch-invariant),
+// not the im2col kernels' (tap, 64-channel) order, so results differ from them by fp32 rounding.
+// The epilogue is epilogue_vec (bias / residual / GroupNorm statistics of the output) with the
+// tile's 64-pixel wave rows mapped to their image rows.
+// ============================================================================================
+namespace halo {
+constexpr int TR = 4, TC = 64;            // output rows / columns per tile
+constexpr int HR = TR + 2, HC = TC + 2;   // halo rows / columns
+constexpr int HPIX = HR * HC;             // 396 halo pixels
+constexpr int NPIECE = (HPIX * 4 + 63) / 64;  // 1 KB DMA pieces per halo (25)
+constexpr int HBYTES = NPIECE * 1024;     // one halo buffer (the last piece's tail slots read zeros)
+constexpr int BN = 128, NW = 8, NT = NW * 64;
+constexpr int BBYTES = BN * 64;           // one tap's 32-channel weight slice
+constexpr int NB = 3;                     // weight ring depth
+constexpr int AB_MAX = 512;               // input channels whose GroupNorm affine fits the LDS table
+constexpr int LDS = 2 * HBYTES + NB * BBYTES + AB_MAX * 8;
+static_assert(LDS <= 80 * 1024, "two blocks per CU");
+static_assert((TR * TC / 2) * (BN + 4) * 4 <= LDS, "epilogue parking (two passes)");
+__device__ __forceinline__ int sw(int s) { return ((s >> 2) & 1) << 1; }
+
+struct Rows {  // tile row r (wave row r / 64, column r % 64) -> output pixel
+  int base, W;
+  __device__ __forceinline__ int operator()(int r) const { return base + (r >> 6) * W + (r & 63); }
+};
+}  // namespace halo
+
+template <bool GN>
+__global__ __launch_bounds__(512, 2) void conv3x3_halo_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
+                                                               unsigned bytesw) {
+  using namespace halo;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const hbuf = lds;
+  char* const bbuf = lds + 2 * HBYTES;
+  float* const abl = reinterpret_cast<float*>(lds + 2 * HBYTES + NB * BBYTES);
+  const int tn = a.cout / BN;
+  // XCD-aware bijective remap (as conv_dma_body): an XCD owns a contiguous run of tile ids, the N
+  // tiles of one image block adjacent (they share its halo through L2)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (orig >> 3);
+  const int nt = wgid % tn;
+  int sp = wgid / tn;
+  const int tx = sp % tiles_x;
+  sp /= tiles_x;
+  const int ty = sp % tiles_y, img = sp / tiles_y;
+  const int oy0 = ty * TR, ox0 = tx * TC, n0 = nt * BN;
+  const int H = a.h, W = a.w, cin = a.c0;
+  const int ncb = cin >> 5, U = ncb * 9;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;  // wave = (output row, 64-channel half)
+
+  if constexpr (GN) {  // the image's (a, b) table, before any DMA is in flight (plain vmcnt use)
+    const float* src = a.gn_ab + (long)img * cin * 2;
+    for (int i = tid; i < cin * 2; i += NT) abl[i] = src[i];
+  }
+
+  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)bytes0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)a.weight, (short)0, (int)bytesw, 0x00020000);
+
+  // halo pieces of this wave: w, w + 8, w + 16 and (wave 0) 24; the other waves repeat piece w + 16
+  // as their 4th (same bytes to the same slots), so every wave issues 4 and vmcnt stays uniform
+  unsigned hvo[4];
+  int hpo[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = (wave + 8 * k < NPIECE) ? wave + 8 * k : wave + 16;
+    const int sl = p * 16 + (lane >> 2), ph = lane & 3;
+    hpo[k] = p * 1024;
+    hvo[k] = kOOB;
+    if (sl < HPIX) {
+      const int hr = sl / HC, hc = sl - (sl / HC) * HC;
+      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        hvo[k] = (unsigned)((img * H + iy) * W + ix) * (unsigned)(a.ld0 * 2) + (unsigned)((ph ^ sw(sl)) * 16);
+    }
+  }
+  // weight rows of this wave: n = 16 wave + lane / 4, chunk lane % 4
+  unsigned bvo;
+  {
+    const int n = wave * 16 + (lane >> 2), ph = lane & 3;
+    bvo = (n0 + n < a.cout) ? (unsigned)(n0 + n) * (unsigned)(a.wld * 2) + (unsigned)((ph ^ sw(n)) * 16) : kOOB;
+  }
+  auto issue_halo = [&](int cb) {
+    char* dst = hbuf + (cb & 1) * HBYTES;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dma16(rs0, dst + hpo[k], hvo[k], cb * 64);
+  };
+  auto issue_b = [&](int u) {
+    const int cb = u / 9, t = u - (u / 9) * 9;
+    dma16(rsw, bbuf + (u % NB) * BBYTES + wave * 1024, bvo, (t * cin + cb * 32) * 2);
+  };
+  auto transform = [&](int cb) {  // silu?(x * a + b) in place, pixels inside the image only
+    char* hb = hbuf + (cb & 1) * HBYTES;
+    for (int j = tid; j < HPIX * 4; j += NT) {
+      const int sl = j >> 2, ph = j & 3;
+      const int hr = sl / HC, hc = sl - (sl / HC) * HC;
+      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+      if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) continue;
+      const float* ab = abl + (cb * 32 + (ph ^ sw(sl)) * 8) * 2;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(hb + j * 16);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = __builtin_fmaf((float)v[e], ab[2 * e], ab[2 * e + 1]);
+        if (a.gn_silu) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+        o[e] = (bf16)x;
+      }
+      *reinterpret_cast<bf16x8*>(hb + j * 16) = o;
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (GN) __syncthreads();  // the affine table is in LDS (its global loads have drained)
+  issue_halo(0);
+  issue_b(0);
+  issue_b(1);
+  wait_vm<2>();  // this wave's halo pieces
+  __builtin_amdgcn_s_barrier();
+  if constexpr (GN) transform(0);
+
+  const int lr = lane & 15, lq = lane >> 4;
+  const int bsw = (lq ^ sw(lr)) * 16;  // weight rows n = 64 wn + 16 j + lr share sw(lr)
+  for (int u = 0; u < U; ++u) {
+    const int cb = u / 9, t = u - (u / 9) * 9;
+    // this step's weights (and at tap 2 the next halo); younger ops allowed in flight: B(u + 1) and,
+    // at tap 1, the next halo's 4 pieces issued at tap 0
+    const bool more = u + 1 < U;
+    if (t == 1 && cb + 1 < ncb) wait_vm<5>();
+    else if (more) wait_vm<1>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (u + 2 < U) issue_b(u + 2);
+    if (t == 0 && cb + 1 < ncb) issue_halo(cb + 1);
+    if constexpr (GN)
+      if (t == 2 && cb + 1 < ncb) transform(cb + 1);  // landed (waited above); read from step (cb + 1, 0)
+    const char* hb = hbuf + (cb & 1) * HBYTES;
+    const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
+    const int ky = t / 3, kx = t - (t / 3) * 3;
+    bf16x8 bfv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
+    const int s0 = (wm + ky) * HC + kx + lr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int sl = s0 + i * 16;
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(hb + sl * 64 + ((lq ^ sw(sl)) << 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  epilogue_vec<TR * TC, BN, 4, 2, NT, 2>(acc, a, 0, n0, wm, wn, lane, tid, lds,
+                                         Rows{(img * H + oy0) * W + ox0, W});
+}
+
+int g_halo = 1;  // 3x3 halo conv: 0 off, 1 for GroupNorm-input convs (default), 2 for every eligible conv
+
+bool halo_ok(const rdeic_conv_desc* d, const ConvArgs& a) {
+  return d->dtype == 1 && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad_t == 1 && d->pad_l == 1 && !d->up2 &&
+         d->c1 == 0 && d->c0 % 32 == 0 && d->c0 <= halo::AB_MAX && d->cout % halo::BN == 0 && d->ho == d->h &&
+         d->wo == d->w && d->h % halo::TR == 0 && d->w % halo::TC == 0 && a.batch == 1 && d->out_mode == 0 &&
+         d->ld0 % 8 == 0 && ((uintptr_t)d->in0 % 16) == 0 && d->wld % 64 == 0 && epi_vec_ok(a) && a.epi_vec;
+}
+
+// The halo conv over image groups whose input stays inside a 32-bit buffer offset.
+int launch_halo(const rdeic_conv_desc* d, ConvArgs a, hipStream_t s, bool* fused) {
+  using namespace halo;
+  const long ipix = (long)d->h * d->w;
+  const long per = ipix * d->ld0 * 2;
+  const int g = (int)(((1l << 31) - 1) / per);
+  if (g < 1 || (long)d->cout * d->wld * 2 >= (1l << 31)) return -1;
+  const bool stats = a.gn_part != nullptr && d->gn_hw == ipix;
+  if (fused) *fused = stats;
+  if (!stats) a.gn_part = nullptr;
+  const int osz = a.out_f32 ? 4 : 2;
+  for (int i0 = 0; i0 < d->n; i0 += g) {
+    ConvArgs e = a;
+    e.n = d->n - i0 < g ? d->n - i0 : g;
+    e.M = e.n * d->ho * d->wo;
+    e.in0 = a.in0 + i0 * per;
+    e.out = a.out + i0 * ipix * d->out_ld * osz;
+    e.res = a.res ? a.res + i0 * ipix * d->res_ld * osz : nullptr;
+    e.emb = a.emb ? a.emb + (long)i0 * a.emb_ld : nullptr;
+    e.gn_ab = a.gn_ab ? a.gn_ab + (long)i0 * d->c0 * 2 : nullptr;
+    e.gn_row0 = i0 * (int)ipix;
+    const unsigned b0 = (unsigned)(((e.n * ipix - 1) * d->ld0 + d->c0) * 2);
+    const unsigned bw = (unsigned)((long)d->cout * d->wld * 2);
+    const int tx = d->w / TC, ty = d->h / TR;
+    const long tiles = (long)e.n * ty * tx * (d->cout / BN);
+    if (e.gn_ab)
+      hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
+    else
+      hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
+    const int rc = launch_status();
+    if (rc != RDEIC_OK) return rc;
+  }
+  return RDEIC_OK;
+}
+
 }  // namespace
 
 namespace {
@@ -1239,6 +1470,12 @@ static int conv2d_run(const rdeic_conv_desc* d, void* stream, bool* fused) {
     return rc2 == -1 ? RDEIC_EINVAL : rc2;
   }
 
+  if (vec && g_halo && (d->gn_ab || g_halo == 2) && halo_ok(d, a)) {
+    a.gn_part = part;
+    const int rc2 = launch_halo(d, a, s, fused);
+    if (rc2 != -1) return rc2;
+    a.gn_part = nullptr;
+  }
   if (d->dtype == 1 && vec && d->cout <= 4 && d->c0 % 32 == 0 && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad_t == 1 &&
       d->pad_l == 1 && !d->up2 && !d->c1 && d->out_mode == 0 && a.batch == 1 && d->ho == d->h && d->wo == d->w &&
       g_conv_path != 0)
@@ -1405,5 +1642,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 3) { int prev = g_swz; g_swz = value; return prev; }
   if (key == 4) { int prev = g_force_tile; g_force_tile = value; return prev; }
   if (key == 5) { int prev = g_dma; g_dma = value; return prev; }
+  if (key == 6) { int prev = g_halo; g_halo = value; return prev; }
   return RDEIC_EINVAL;
 }

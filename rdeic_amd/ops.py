@@ -98,7 +98,8 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     stats: the output feeds a GroupNorm — its statistics are produced with it (fused into the conv
     epilogue where the tile allows, rdeic_conv_desc.gn_part) and group_norm_ab(out) then needs no
     pass over the tensor. stats_hw: pixels per image of that GroupNorm (default ho*wo)."""
-    if gn is not None and _gn_materialize(x, x2, p):
+    if gn is not None and _gn_materialize(x, x2, p) and not _halo_eligible(x, x2, p, up2, pad_t, pad_l, out_hw,
+                                                                           geglu or pixel_shuffle, out):
         # the big-tile conv path has no GroupNorm prologue (it is VALU-bound there): materialise the
         # normalised (concatenated) input once with the vectorised, HBM-rate apply kernel instead
         xin = torch.empty(x.shape[:3] + (p.cin,), dtype=x.dtype, device=x.device)
@@ -467,6 +468,37 @@ def set_conv_path(path: int) -> int:
 def set_conv_option(key: int, value: int) -> int:
     """rdeic_set_conv_option: key 0 vectorised epilogue, 1 dh=64 attention kernel, 2 two-deep prefetch."""
     return int(_lib.load().rdeic_set_conv_option(int(key), int(value)))
+
+
+# 3x3 halo conv (rdeic_amd/csrc/conv_gemm.hip, conv3x3_halo_kernel): a conv whose input is a
+# GroupNorm (+ SiLU) of a single 32-channel-aligned NHWC tensor and whose output tiles as 4 x 64 pixel
+# blocks x 128 channels takes the raw input and applies the affine once per element in LDS, instead
+# of materialising the normalised tensor (rdeic_set_conv_option(6, .): 0 off, 1 GroupNorm inputs, 2 all).
+HALO_CONV = 1
+
+
+def set_halo_conv(mode: int) -> int:
+    global HALO_CONV
+    prev = HALO_CONV
+    HALO_CONV = int(mode)
+    _lib.load().rdeic_set_conv_option(6, HALO_CONV)
+    return prev
+
+
+def _halo_eligible(x, x2, p: "ConvParams", up2, pad_t, pad_l, out_hw, special, out) -> bool:
+    """Mirror of the library's halo_ok (the conv2d_run dispatch) for a GroupNorm-input conv."""
+    if not HALO_CONV or x.dtype != torch.bfloat16 or x2 is not None or up2 or special:
+        return False
+    if p.kh != 3 or p.kw != 3 or p.stride != 1 or p.pad != 1 or (pad_t not in (None, 1)) or (pad_l not in (None, 1)):
+        return False
+    n, h, w, c = x.shape
+    if out_hw is not None and tuple(out_hw) != (h, w):
+        return False
+    if c % 32 or c > 512 or p.cout % 128 or h % 4 or w % 64 or x.stride(2) % 8 or x.data_ptr() % 16:
+        return False
+    if out is not None and (pix_ld(out) % 8 or out.data_ptr() % 16):
+        return False
+    return True
 
 
 def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) -> bool:

@@ -4,8 +4,9 @@ match the reference (tests/test_config2_gpu.py); bf16 computes mu / sigma and th
 so its symbols and pixels differ. The north star asks for "bpp equal to reference": this bounds
 the gap per image and on the batch, and prints the measured values.
 
-Bounds (measured on MI355X, with margin): mean bpp within 3% and every image within 8%; mean PSNR
-(decoded vs input) within 0.3 dB; mean MS-SSIM within 0.01."""
+Measured on MI355X (r03, the bench's 16 images): bf16 mean bpp +0.29% over fp32, worst image
+1.1%; mean PSNR +0.0025 dB; mean MS-SSIM -4e-5. Bounds, with margin: mean bpp within 1.5% and every
+image within 5%; mean PSNR (decoded vs input) within 0.1 dB; mean MS-SSIM within 0.003."""
 import numpy as np
 import pytest
 import torch
@@ -42,7 +43,7 @@ def test_bf16_vs_fp32_bpp_and_quality(gpu):
           f"per-image max |rel| {np.abs(rel).max():.4f})")
     print(f"PSNR fp32 {p32.mean():.3f} bf16 {p16.mean():.3f} dB (delta {p16.mean() - p32.mean():+.3f}); "
           f"MS-SSIM fp32 {s32.mean():.5f} bf16 {s16.mean():.5f} (delta {s16.mean() - s32.mean():+.5f})")
-    assert abs(b16.mean() - b32.mean()) <= 0.03 * b32.mean()
-    assert np.abs(rel).max() <= 0.08
-    assert abs(p16.mean() - p32.mean()) <= 0.3
-    assert abs(s16.mean() - s32.mean()) <= 0.01
+    assert abs(b16.mean() - b32.mean()) <= 0.015 * b32.mean()
+    assert np.abs(rel).max() <= 0.05
+    assert abs(p16.mean() - p32.mean()) <= 0.1
+    assert abs(s16.mean() - s32.mean()) <= 0.003
