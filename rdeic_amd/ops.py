@@ -475,6 +475,10 @@ def set_conv_option(key: int, value: int) -> int:
 # blocks x 128 channels takes the raw input and applies the affine once per element in LDS, instead
 # of materialising the normalised tensor (rdeic_set_conv_option(6, .): 0 off, 1 GroupNorm inputs, 2 all).
 HALO_CONV = 1
+# widest input / output the halo conv takes over from the materialised path: measured at B=16
+# (tools/halo_bench.py) it wins on the 512^2 128-channel layers (2.17 -> 1.72 ms, 3.72 -> 3.01 ms), ties
+# at 256^2 x 256, and loses to the 256x256 im2col tiles on the 512-channel layers
+HALO_MAX_C = 256
 
 
 def set_halo_conv(mode: int) -> int:
@@ -494,7 +498,8 @@ def _halo_eligible(x, x2, p: "ConvParams", up2, pad_t, pad_l, out_hw, special, o
     n, h, w, c = x.shape
     if out_hw is not None and tuple(out_hw) != (h, w):
         return False
-    if c % 32 or c > 512 or p.cout % 128 or h % 4 or w % 64 or x.stride(2) % 8 or x.data_ptr() % 16:
+    if c % 32 or c > min(512, HALO_MAX_C) or p.cout > HALO_MAX_C or p.cout % 128 or h % 4 or w % 64 \
+            or x.stride(2) % 8 or x.data_ptr() % 16:
         return False
     if out is not None and (pix_ld(out) % 8 or out.data_ptr() % 16):
         return False
