@@ -1298,24 +1298,45 @@ __global__ __launch_bounds__(512, 2) void conv3x3_halo_kernel(ConvArgs a, int ti
     const int cb = u / 9, t = u - (u / 9) * 9;
     dma16(rsw, bbuf + (u % NB) * BBYTES + wave * 1024, bvo, (t * cin + cb * 32) * 2);
   };
-  auto transform = [&](int cb) {  // silu?(x * a + b) in place, pixels inside the image only
+  // The in-place GroupNorm (+ SiLU) of a halo: every wave transforms exactly the chunks its own
+  // DMA pieces brought in (one 16-byte chunk per lane per piece; the duplicate 4th piece of waves
+  // 1..7 is skipped), right after its own counted vmcnt: no barrier between landing and transform.
+  // Pixels outside the image (the conv's zero padding of the normalised tensor) stay zero.
+  bool hown[4];
+  int hch[4];  // logical channel chunk (0..3) of this lane's chunk in piece k
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = (wave + 8 * k < NPIECE) ? wave + 8 * k : -1;
+    const int sl = (p < 0 ? 0 : p) * 16 + (lane >> 2);
+    hown[k] = p >= 0 && hvo[k] != kOOB;
+    hch[k] = (lane & 3) ^ sw(sl);
+  }
+  auto transform = [&](int cb) {
     char* hb = hbuf + (cb & 1) * HBYTES;
-    for (int j = tid; j < HPIX * 4; j += NT) {
-      const int sl = j >> 2, ph = j & 3;
-      const int hr = sl / HC, hc = sl - (sl / HC) * HC;
-      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
-      if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) continue;
-      const float* ab = abl + (cb * 32 + (ph ^ sw(sl)) * 8) * 2;
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(hb + j * 16);
+    bf16x8 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (hown[k]) v[k] = *reinterpret_cast<const bf16x8*>(hb + hpo[k] + lane * 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!hown[k]) continue;
+      const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + hch[k] * 8) * 2);
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = __builtin_fmaf((float)v[e], ab[2 * e], ab[2 * e + 1]);
-        if (a.gn_silu) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
-        o[e] = (bf16)x;
+      for (int q = 0; q < 4; ++q) {
+        const float4 ab = ab4[q];  // (a, b) of channels 2q, 2q + 1 of the chunk
+        float x0 = __builtin_fmaf((float)v[k][2 * q], ab.x, ab.y);
+        float x1 = __builtin_fmaf((float)v[k][2 * q + 1], ab.z, ab.w);
+        if (a.gn_silu) {
+          x0 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x0));
+          x1 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x1));
+        }
+        o[2 * q] = (bf16)x0;
+        o[2 * q + 1] = (bf16)x1;
       }
-      *reinterpret_cast<bf16x8*>(hb + j * 16) = o;
+      *reinterpret_cast<bf16x8*>(hb + hpo[k] + lane * 16) = o;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
   };
 
   f32x4 acc[4][4];
@@ -1329,7 +1350,6 @@ __global__ __launch_bounds__(512, 2) void conv3x3_halo_kernel(ConvArgs a, int ti
   issue_b(0);
   issue_b(1);
   wait_vm<2>();  // this wave's halo pieces
-  __builtin_amdgcn_s_barrier();
   if constexpr (GN) transform(0);
 
   const int lr = lane & 15, lq = lane >> 4;
@@ -1342,11 +1362,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_halo_kernel(ConvArgs a, int ti
     if (t == 1 && cb + 1 < ncb) wait_vm<5>();
     else if (more) wait_vm<1>();
     else wait_vm<0>();
+    if constexpr (GN)
+      if (t == 2 && cb + 1 < ncb) transform(cb + 1);  // own pieces landed (waited above); read from (cb + 1, 0)
     __builtin_amdgcn_s_barrier();
     if (u + 2 < U) issue_b(u + 2);
     if (t == 0 && cb + 1 < ncb) issue_halo(cb + 1);
-    if constexpr (GN)
-      if (t == 2 && cb + 1 < ncb) transform(cb + 1);  // landed (waited above); read from step (cb + 1, 0)
     const char* hb = hbuf + (cb & 1) * HBYTES;
     const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
     const int ky = t / 3, kx = t - (t / 3) * 3;

@@ -8,6 +8,3 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 200 python -u tools/halo_bench.py > $O/halo_bench.txt 2>&1
 rc=$?; tail -12 $O/halo_bench.txt
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 python -u tools/probe/c3_determinism.py > $O/c3det.txt 2>&1
-rc=$?; tail -16 $O/c3det.txt
-exit $rc
