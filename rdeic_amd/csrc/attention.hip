@@ -866,6 +866,7 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
 // ============================================================================================
 constexpr int A512_Q = 64, A512_KT = 32, A512_TILE = A512_KT * 1024, A512_STAGE = 2 * A512_TILE;
 
+template <int SYNC>
 __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
                                                       int ldk, const bf16* __restrict__ v, int ldv,
                                                       bf16* __restrict__ o, int ldo, int lq, int lk,
@@ -924,7 +925,9 @@ __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q
   issue(0, 0);
   for (int kt = 0; kt < ntiles; ++kt) {
     attn_wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
+    if constexpr (SYNC == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (SYNC == 2) __syncthreads();
+    else __builtin_amdgcn_s_barrier();
     if (kt + 1 < ntiles) issue(kt + 1, (kt + 1) & 1);
     const char* Kt = lds + (kt & 1) * A512_STAGE;
     const char* Vt = Kt + A512_TILE;
@@ -1029,8 +1032,14 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
           (long)(lk - 1) * (ldk > ldv ? ldk : ldv) * 2 + 1024 >= (1l << 31))
         return RDEIC_EINVAL;
       dim3 grid((lq + A512_Q - 1) / A512_Q, batch);
-      hipLaunchKernelGGL(attn512_kernel, grid, dim3(256), 2 * A512_STAGE, s, (const bf16*)q, ldq, (const bf16*)k, ldk,
-                         (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f);
+      static const int sync = getenv("RDEIC_A512_SYNC") ? atoi(getenv("RDEIC_A512_SYNC")) : 0;  // probe A/B
+#define A512_LAUNCH(S)                                                                                         \
+  hipLaunchKernelGGL(attn512_kernel<S>, grid, dim3(256), 2 * A512_STAGE, s, (const bf16*)q, ldq, (const bf16*)k, ldk, \
+                     (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f)
+      if (sync == 1) A512_LAUNCH(1);
+      else if (sync == 2) A512_LAUNCH(2);
+      else A512_LAUNCH(0);
+#undef A512_LAUNCH
       return launch_status();
     }
     if (dh == 64 && rdeic_g_attn64 == 2 && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 &&
