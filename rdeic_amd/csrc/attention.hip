@@ -928,6 +928,10 @@ __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q
     if constexpr (SYNC == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (SYNC == 2) __syncthreads();
     else __builtin_amdgcn_s_barrier();
+    if constexpr (SYNC == 4) {  // a second full barrier: every wave past the first one
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     if (kt + 1 < ntiles) issue(kt + 1, (kt + 1) & 1);
     const char* Kt = lds + (kt & 1) * A512_STAGE;
     const char* Vt = Kt + A512_TILE;
@@ -993,7 +997,8 @@ __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q
         const unsigned a = vaddr(dt + VD - 1);
         vt[(dt + VD - 1) % VD][0] = ds_read_tr16_off<0>(a);
         vt[(dt + VD - 1) % VD][1] = ds_read_tr16_off<16 * 1024>(a);
-        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * (VD - 1)) : "memory");
+        if constexpr (SYNC == 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * (VD - 1)) : "memory");
       } else if (dt + 2 < 32) {
         asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
       } else if (dt + 1 < 32) {
@@ -1038,6 +1043,8 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
                      (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f)
       if (sync == 1) A512_LAUNCH(1);
       else if (sync == 2) A512_LAUNCH(2);
+      else if (sync == 3) A512_LAUNCH(3);
+      else if (sync == 4) A512_LAUNCH(4);
       else A512_LAUNCH(0);
 #undef A512_LAUNCH
       return launch_status();
