@@ -643,6 +643,13 @@ __device__ __forceinline__ v4s ds_read_tr16_off(unsigned lds_addr) {
   return r;
 }
 
+// A counted lgkmcnt wait does not order anything for the compiler: an MFMA that reads the result
+// of an asm transposed read has no dependence on the wait asm and may be scheduled above it, reading
+// the VGPRs before the LDS data has arrived (rare, timing-dependent wrong values; measured on
+// attn512 at L = 16384: 6-8 of 59 repeats differed). tie() passes the registers through an empty
+// volatile asm placed after the wait, so every consumer is data-dependent on a point past it.
+__device__ __forceinline__ void tie(v4s& a) { asm volatile("" : "+v"(a)); }
+
 template <int N>
 __device__ __forceinline__ void attn_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -815,6 +822,13 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm transposed reads above
 #pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        tie(vt[dt][c][0]);  // consumers past the wait
+        tie(vt[dt][c][1]);
+      }
+#pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -866,7 +880,6 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
 // ============================================================================================
 constexpr int A512_Q = 64, A512_KT = 32, A512_TILE = A512_KT * 1024, A512_STAGE = 2 * A512_TILE;
 
-template <int SYNC>
 __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
                                                       int ldk, const bf16* __restrict__ v, int ldv,
                                                       bf16* __restrict__ o, int ldo, int lq, int lk,
@@ -925,13 +938,7 @@ __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q
   issue(0, 0);
   for (int kt = 0; kt < ntiles; ++kt) {
     attn_wait_vm<0>();
-    if constexpr (SYNC == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (SYNC == 2) __syncthreads();
-    else __builtin_amdgcn_s_barrier();
-    if constexpr (SYNC == 4) {  // a second full barrier: every wave past the first one
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
+    __builtin_amdgcn_s_barrier();
     if (kt + 1 < ntiles) issue(kt + 1, (kt + 1) & 1);
     const char* Kt = lds + (kt & 1) * A512_STAGE;
     const char* Vt = Kt + A512_TILE;
@@ -997,8 +1004,7 @@ __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q
         const unsigned a = vaddr(dt + VD - 1);
         vt[(dt + VD - 1) % VD][0] = ds_read_tr16_off<0>(a);
         vt[(dt + VD - 1) % VD][1] = ds_read_tr16_off<16 * 1024>(a);
-        if constexpr (SYNC == 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * (VD - 1)) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * (VD - 1)) : "memory");
       } else if (dt + 2 < 32) {
         asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
       } else if (dt + 1 < 32) {
@@ -1006,6 +1012,8 @@ __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q
       } else {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
+      tie(vt[cb][0]);  // the MFMA below stays past the counted wait above
+      tie(vt[cb][1]);
       const v4s both[2] = {vt[cb][0], vt[cb][1]};
       const bf16x8 vf = *reinterpret_cast<const bf16x8*>(both);
       oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, oacc[dt], 0, 0, 0);
@@ -1037,16 +1045,8 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
           (long)(lk - 1) * (ldk > ldv ? ldk : ldv) * 2 + 1024 >= (1l << 31))
         return RDEIC_EINVAL;
       dim3 grid((lq + A512_Q - 1) / A512_Q, batch);
-      static const int sync = getenv("RDEIC_A512_SYNC") ? atoi(getenv("RDEIC_A512_SYNC")) : 0;  // probe A/B
-#define A512_LAUNCH(S)                                                                                         \
-  hipLaunchKernelGGL(attn512_kernel<S>, grid, dim3(256), 2 * A512_STAGE, s, (const bf16*)q, ldq, (const bf16*)k, ldk, \
-                     (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f)
-      if (sync == 1) A512_LAUNCH(1);
-      else if (sync == 2) A512_LAUNCH(2);
-      else if (sync == 3) A512_LAUNCH(3);
-      else if (sync == 4) A512_LAUNCH(4);
-      else A512_LAUNCH(0);
-#undef A512_LAUNCH
+      hipLaunchKernelGGL(attn512_kernel, grid, dim3(256), 2 * A512_STAGE, s, (const bf16*)q, ldq, (const bf16*)k, ldk,
+                         (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f);
       return launch_status();
     }
     if (dh == 64 && rdeic_g_attn64 == 2 && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 &&

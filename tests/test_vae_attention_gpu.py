@@ -57,3 +57,24 @@ def test_flash_d512_matches_fp32_reference(gpu, B, L, spread):
         mat = torch.empty_like(out)
         ops.attention_single_head_materialized(q, k, v, mat, batch=B, length=L, dim=C, scale=scale)
         assert (mat.float() - out.float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("dh,heads,B,L,reps", [(512, 1, 8, 16384, 24), (64, 5, 8, 16384, 24), (64, 5, 16, 4096, 24)])
+def test_flash_kernels_run_to_run_deterministic(gpu, dh, heads, B, L, reps):
+    """Repeated launches on the same inputs give the same bits (config 3's 1024^2 shapes). The asm
+    transposed V reads of attn512 / attn64 are ordered after their counted lgkmcnt waits only by
+    data dependence (attention.hip tie()); without it the MFMA could read a VGPR before its LDS
+    data arrived: 6-8 of 59 repeats differed at B=8, L=16384 (tools/probe/attn512_repeat.py)."""
+    from rdeic_amd import ops
+    C = heads * dh
+    g = torch.Generator(device="cuda").manual_seed(L + dh)
+    qkv = torch.randn(B * L, 3 * C, device="cuda", generator=g).to(torch.bfloat16)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    ref = torch.empty(B * L, C, dtype=torch.bfloat16, device="cuda")
+    ops.attention(q, k, v, ref, batch=B, heads=heads, lq=L, lk=L, dh=dh, scale=dh ** -0.5)
+    bad = 0
+    for _ in range(reps):
+        o = torch.empty_like(ref)
+        ops.attention(q, k, v, o, batch=B, heads=heads, lq=L, lk=L, dh=dh, scale=dh ** -0.5)
+        bad += int(not torch.equal(o, ref))
+    assert bad == 0, f"{bad}/{reps} repeats differ"
