@@ -278,7 +278,21 @@ class Compression:
         return self._plans.run(key, fn, inputs, before=before)
 
     # ------------------------------------------------------------------ compress / decompress
+    def _splitk(self):
+        """Split-K for the entropy model's small-grid convs (bf16; ops.SPLITK_ENTROPY): the k-split count
+        is chosen from the per-image shape (ops.SPLITK_NOMINAL_BATCH), so the encoder and the decoder —
+        whatever their batch — run every layer with the same k grouping and compute identical mu / sigma.
+        The fp32 parity mode keeps the unsplit order of the oracle comparison."""
+        import contextlib
+        if self.store.compute_dtype == torch.bfloat16 and ops.SPLITK_ENTROPY:
+            return ops.splitk_allowed()
+        return contextlib.nullcontext()
+
     def _compress_gpu(self, h: torch.Tensor) -> torch.Tensor:
+        with self._splitk():
+            return self._compress_gpu_body(h)
+
+    def _compress_gpu_body(self, h: torch.Tensor) -> torch.Tensor:
         """compress() up to the bytes of the z indexes: nets, VQ, the 20 stages, and (host steps)
         the rANS coding of each image group into self._io["y_strings"]. Returns the pinned host
         copy of the VQ indexes [B, hz, wz], complete once the region has run."""
@@ -357,6 +371,10 @@ class Compression:
         return self.compress_with(lambda t: t, h)
 
     def _decompress_gpu(self, z_idx: torch.Tensor):
+        with self._splitk():
+            return self._decompress_gpu_body(z_idx)
+
+    def _decompress_gpu_body(self, z_idx: torch.Tensor):
         """decompress() from the device VQ indexes on: codebook, hyper decoder, the 20 stages with
         their rANS round trips (host steps, decoders in self._io["decs"]), g_s and the out conv."""
         B, hz, wz = z_idx.shape

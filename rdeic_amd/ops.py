@@ -302,6 +302,8 @@ SPLITK_SHORT = False  # training: also split the short-K (k-tiles >= 8) small-M 
 # batch (bench, CLI --batch_size / --micro_batch_size, data-parallel shards). Training (SPLITK_SHORT,
 # B=1) sizes splits from the real M: it needs no batch invariance.
 SPLITK_NOMINAL_BATCH = 16
+# bf16 entropy model (Compression nets at the y / z resolution): split-K allowed, per-image counts
+SPLITK_ENTROPY = True
 
 
 class splitk_allowed:
