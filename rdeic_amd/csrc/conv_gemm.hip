@@ -1233,7 +1233,7 @@ struct Rows {  // tile row r (wave row r / 64, column r % 64) -> output pixel
 }  // namespace halo
 
 template <bool GN>
-__global__ __launch_bounds__(512, 2) void conv3x3_halo_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3x3_halo_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
                                                                unsigned bytesw) {
   using namespace halo;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -1302,39 +1302,44 @@ __global__ __launch_bounds__(512, 2) void conv3x3_halo_kernel(ConvArgs a, int ti
   // DMA pieces brought in (one 16-byte chunk per lane per piece; the duplicate 4th piece of waves
   // 1..7 is skipped), right after its own counted vmcnt: no barrier between landing and transform.
   // Pixels outside the image (the conv's zero padding of the normalised tensor) stay zero.
-  bool hown[4];
-  int hch[4];  // logical channel chunk (0..3) of this lane's chunk in piece k
+  // per piece k: bit k = this lane's chunk is inside the image (transform it), bits 4 + 2k: its
+  // logical channel chunk (one VGPR for all four pieces)
+  unsigned hinfo = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int p = (wave + 8 * k < NPIECE) ? wave + 8 * k : -1;
     const int sl = (p < 0 ? 0 : p) * 16 + (lane >> 2);
-    hown[k] = p >= 0 && hvo[k] != kOOB;
-    hch[k] = (lane & 3) ^ sw(sl);
+    if (p >= 0 && hvo[k] != kOOB) hinfo |= 1u << k;
+    hinfo |= (unsigned)((lane & 3) ^ sw(sl)) << (4 + 2 * k);
   }
   auto transform = [&](int cb) {
-    char* hb = hbuf + (cb & 1) * HBYTES;
-    bf16x8 v[4];
+    char* hb = hbuf + (cb & 1) * HBYTES + lane * 16;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (hown[k]) v[k] = *reinterpret_cast<const bf16x8*>(hb + hpo[k] + lane * 16);
+    for (int k0 = 0; k0 < 4; k0 += 2) {  // two chunks in flight at a time (register budget)
+      bf16x8 v[2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (!hown[k]) continue;
-      const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + hch[k] * 8) * 2);
-      bf16x8 o;
+      for (int k = k0; k < k0 + 2; ++k)
+        if (hinfo & (1u << k)) v[k - k0] = *reinterpret_cast<const bf16x8*>(hb + hpo[k]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 ab = ab4[q];  // (a, b) of channels 2q, 2q + 1 of the chunk
-        float x0 = __builtin_fmaf((float)v[k][2 * q], ab.x, ab.y);
-        float x1 = __builtin_fmaf((float)v[k][2 * q + 1], ab.z, ab.w);
-        if (a.gn_silu) {
-          x0 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x0));
-          x1 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x1));
+      for (int k = k0; k < k0 + 2; ++k) {
+        if (!(hinfo & (1u << k))) continue;
+        const int ch = (hinfo >> (4 + 2 * k)) & 3;
+        const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 ab = ab4[q];  // (a, b) of channels 2q, 2q + 1 of the chunk
+          float x0 = __builtin_fmaf((float)v[k - k0][2 * q], ab.x, ab.y);
+          float x1 = __builtin_fmaf((float)v[k - k0][2 * q + 1], ab.z, ab.w);
+          if (a.gn_silu) {
+            x0 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x0));
+            x1 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x1));
+          }
+          o[2 * q] = (bf16)x0;
+          o[2 * q + 1] = (bf16)x1;
         }
-        o[2 * q] = (bf16)x0;
-        o[2 * q + 1] = (bf16)x1;
+        *reinterpret_cast<bf16x8*>(hb + hpo[k]) = o;
       }
-      *reinterpret_cast<bf16x8*>(hb + hpo[k] + lane * 16) = o;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
   };
@@ -1354,32 +1359,50 @@ __global__ __launch_bounds__(512, 2) void conv3x3_halo_kernel(ConvArgs a, int ti
 
   const int lr = lane & 15, lq = lane >> 4;
   const int bsw = (lq ^ sw(lr)) * 16;  // weight rows n = 64 wn + 16 j + lr share sw(lr)
-  for (int u = 0; u < U; ++u) {
-    const int cb = u / 9, t = u - (u / 9) * 9;
-    // this step's weights (and at tap 2 the next halo); younger ops allowed in flight: B(u + 1) and,
-    // at tap 1, the next halo's 4 pieces issued at tap 0
-    const bool more = u + 1 < U;
-    if (t == 1 && cb + 1 < ncb) wait_vm<5>();
-    else if (more) wait_vm<1>();
-    else wait_vm<0>();
-    if constexpr (GN)
-      if (t == 2 && cb + 1 < ncb) transform(cb + 1);  // own pieces landed (waited above); read from (cb + 1, 0)
-    __builtin_amdgcn_s_barrier();
-    if (u + 2 < U) issue_b(u + 2);
-    if (t == 0 && cb + 1 < ncb) issue_halo(cb + 1);
+  // A fragment i of a tap reads halo slots s0 + 16 i + lr: adding 16 leaves bits 0..3 (and so the
+  // swizzle) unchanged, so one lane address per tap serves all four fragments (immediate offsets)
+  // taps unrolled: ring slot (u % 3 = t % 3, 9 taps per block), filter offset, waits and the next
+  // loads are compile-time per tap; the only runtime branch is "is there a next channel block"
+  for (int cb = 0; cb < ncb; ++cb) {
+    const bool more = cb + 1 < ncb;
     const char* hb = hbuf + (cb & 1) * HBYTES;
-    const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
-    const int ky = t / 3, kx = t - (t / 3) * 3;
-    bf16x8 bfv[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
-    const int s0 = (wm + ky) * HC + kx + lr;
+    for (int t = 0; t < 9; ++t) {
+      // this tap's weights (and at tap 2 the next halo); younger ops allowed in flight: the next tap's
+      // weights and, at tap 1, the next halo's 4 pieces issued at tap 0
+      if (t == 1) {
+        if (more) wait_vm<5>(); else wait_vm<1>();
+      } else if (t < 8 || more) {
+        wait_vm<1>();
+      } else {
+        wait_vm<0>();
+      }
+      if constexpr (GN)
+        if (t == 2 && more) transform(cb + 1);  // own pieces landed (waited above); read from (cb + 1, 0)
+      __builtin_amdgcn_s_barrier();
+      if (t + 2 < 9) {
+        dma16(rsw, bbuf + ((t + 2) % NB) * BBYTES + wave * 1024, bvo, ((t + 2) * cin + cb * 32) * 2);
+      } else if (more) {
+        dma16(rsw, bbuf + ((t + 2) % NB) * BBYTES + wave * 1024, bvo, ((t + 2 - 9) * cin + (cb + 1) * 32) * 2);
+      }
+      if (t == 0 && more) issue_halo(cb + 1);
+      const char* bb = bbuf + (t % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
+      const int ky = t / 3, kx = t - (t / 3) * 3;
+      bf16x8 bfv[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int sl = s0 + i * 16;
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(hb + sl * 64 + ((lq ^ sw(sl)) << 4));
+      for (int j = 0; j < 4; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
+      // per-tap lane address, recomputed each tap from a laundered base (the compiler would otherwise
+      // hoist all 9 taps' addresses out of the channel-block loop and spill)
+      int lb = wm * HC + lr;
+      asm volatile("" : "+v"(lb));
+      const int sl = lb + ky * HC + kx;
+      const char* ab = hb + sl * 64 + ((lq ^ sw(sl)) << 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+      }
     }
   }
   epilogue_vec<TR * TC, BN, 4, 2, NT, 2>(acc, a, 0, n0, wm, wn, lane, tid, lds,
