@@ -478,9 +478,10 @@ def set_conv_option(key: int, value: int) -> int:
 # of materialising the normalised tensor (rdeic_set_conv_option(6, .): 0 off, 1 GroupNorm inputs, 2 all).
 HALO_CONV = 1
 # widest input / output the halo conv takes over from the materialised path: measured at B=16
-# (tools/halo_bench.py) it wins on the 512^2 128-channel layers (2.17 -> 1.72 ms, 3.72 -> 3.01 ms), ties
-# at 256^2 x 256, and loses to the 256x256 im2col tiles on the 512-channel layers
-HALO_MAX_C = 256
+# (tools/halo_bench.py, r03) it wins on the 512^2 128-channel layers (2.14 -> 1.53 ms, 3.59 -> 2.62 ms)
+# and the 256^2 ones (0.86 -> 0.75, 1.39 -> 1.26 ms) and ties the 256x256 im2col tiles on the
+# 512-channel layers at 128^2 / 64^2 (where it still saves the GroupNorm apply launches)
+HALO_MAX_C = 512
 
 
 def set_halo_conv(mode: int) -> int:
