@@ -23,6 +23,7 @@ import sys
 
 FAMILIES = [  # (family, substring on the demangled name), first match wins
     ("conv", "conv_dma_kernel"), ("conv", "conv_kernel"), ("conv", "conv3x3_smallc"), ("conv", "splitk_reduce"),
+    ("conv", "conv3x3_halo"),
     ("conv", "conv_out_dot2"),
     ("attention", "attn"), ("vae_attention_softmax", "softmax_rows"),
     ("groupnorm", "gn_"), ("layernorm", "layernorm"),
