@@ -35,6 +35,20 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 // exact-erf GELU (torch.nn.GELU / F.gelu default)
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// GELU with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 on erf): one rcp and one exp instead
+// of the library erff's range split. For bf16 outputs only (the fused GEGLU projection epilogue);
+// fp32 parity paths keep gelu_f.
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, z, 1.0f));
+  float p = __builtin_fmaf(1.061405429f, t, -1.453152027f);
+  p = __builtin_fmaf(p, t, 1.421413741f);
+  p = __builtin_fmaf(p, t, -0.284496736f);
+  p = __builtin_fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = 1.0f - p * __expf(-z * z);  // erf(|x| / sqrt 2)
+  return 0.5f * x * (1.0f + copysignf(e, x));
+}
 
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll

@@ -195,7 +195,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float xv = to_f32(from_f32<bf16>(v[e])), gt = to_f32(from_f32<bf16>(v[4 + e]));
-          gv[e] = from_f32<bf16>(xv * gelu_f(gt));
+          gv[e] = from_f32<bf16>(xv * gelu_fast(gt));
         }
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + (nn >> 1)) =
             *reinterpret_cast<uint2*>(gv);
