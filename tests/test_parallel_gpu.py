@@ -90,3 +90,42 @@ def test_two_rank_sharded_codec_matches_single_process(gpu):
         assert gathered[:, 2].tolist() == list(range(G))  # global image order
         assert gathered[:, 1].tolist() == [float(len(b)) for b in bodies_all]
         assert gathered[:, 3].tolist() == [float(o) for o in range(WORLD) for _ in range(*parallel.shard(G, o, WORLD))]
+
+
+def _nccl_rank(port, q):
+    try:
+        import torch.distributed as dist
+        from rdeic_amd import parallel
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        torch.cuda.set_device(0)
+        dist.init_process_group(backend="nccl")  # RCCL on ROCm
+        dev = torch.device("cuda", 0)
+        rows = torch.arange(12, dtype=torch.float32, device=dev).view(3, 4)
+        out = torch.empty_like(rows)
+        dist.all_gather_into_tensor(out, rows)  # the metric gather's collective, on RCCL
+        t = torch.tensor([2.5], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py's max-over-ranks timing
+        g = torch.ones(1000, device=dev)
+        h = dist.all_reduce(g, async_op=True)  # GradBuckets' async bucket all-reduce
+        h.wait()
+        parallel.barrier(dev)
+        q.put((torch.equal(out, rows), float(t.item()), float(g.sum().item()), dist.get_backend()))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((False, f"{type(e).__name__}: {e}", 0.0, None))
+
+
+def test_rccl_collectives_single_rank(gpu):
+    """The RCCL ("nccl") process group the multi-GPU bench / fine-tune use, exercised on the one
+    visible GPU (RCCL refuses two ranks on one device, so the two-rank tests above use gloo): the
+    metric all_gather_into_tensor, the timing all_reduce(MAX), an async all_reduce and the device
+    barrier run and return the identity results at world size 1."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_rank, args=(_free_port(), q))
+    p.start()
+    ok, t, s, backend = q.get(timeout=180)
+    p.join(timeout=60)
+    assert ok is True, t
+    assert t == 2.5 and s == 1000.0 and backend == "nccl"
+    assert p.exitcode == 0
