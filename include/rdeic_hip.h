@@ -107,8 +107,11 @@ int rdeic_set_conv_path(int32_t path);
  * key 3: XOR-swizzled 128-byte LDS rows on the <= 8-wave conv tiles (1 default) / padded rows (0);
  * key 4: force the big-tile candidate (0 256x256, 1 256x128, 2 128x256, 3 128x128, 4 64x128,
  *        5 128x64; -1 = automatic choice, default) — tuning only;
- * key 5: LDS-DMA conv kernel for 64-channel-aligned layers on (1, default) / off (0).
- * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way. */
+ * key 5: LDS-DMA conv kernel for 64-channel-aligned layers on (1, default) / off (0);
+ * key 6: halo-strip 3x3 conv with the GroupNorm applied in LDS: 0 off, 1 GroupNorm-input convs
+ *        (default), 2 every eligible conv (its k order differs from the im2col tiles');
+ * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way
+ * (keys 0-5). */
 int rdeic_set_conv_option(int32_t key, int32_t value);
 
 /* --------------------------------------------------------- normalisation

@@ -149,10 +149,16 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
   // squares), combined as ((g0 + g1) + g2) + g3 — exactly what gn_rows_partial_kernel computes, so
   // the statistics (and every GroupNorm after them) are identical for every tile and batch size.
   // Each pass writes its stored values back over its parked accumulators; thread (b, j) then scans
-  // column j of 64-row block b in LDS. Needs WTM in {32, 64} (a wave-row block inside one 64-row
-  // block) and (BM / 64) * BN <= NT; the host enables it only for such tiles (stats_tile_ok).
+  // column j of 64-row block b in LDS (NU such pairs per thread when the tile has more pairs than
+  // threads). Needs WTM in {32, 64} (a wave-row block inside one 64-row block); the host enables it
+  // only for such tiles (stats_tile_ok).
   const bool st = a.gn_part != nullptr;
-  float sg[4] = {0.f, 0.f, 0.f, 0.f}, qg[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NU = ((BM / 64) * BN + NT - 1) / NT;  // (64-row block, channel) pairs per thread
+  float sg[NU][4], qg[NU][4];
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) sg[u][g] = qg[u][g] = 0.f;
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     __syncthreads();
@@ -234,10 +240,12 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
         }
       }
     }
-    if constexpr ((WTM == 32 || WTM == 64) && (BM / 64) * BN <= NT && (WTM / P) % 16 == 0) {
+    if constexpr ((WTM == 32 || WTM == 64) && (WTM / P) % 16 == 0) {
       if (st) {
         __syncthreads();
-        const int b = tid / BN, j = tid - (tid / BN) * BN;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+        const int b = (tid + u * NT) / BN, j = (tid + u * NT) % BN;
         if (b < BM / 64) {
           constexpr int WPB = 64 / WTM;  // wave-row blocks per 64-row block
 #pragma unroll
@@ -258,22 +266,26 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
               } else {
                 for (int r = 0; r < nv; ++r) { const float y = col[r * SDW]; s1 += y; s2 = fmaf(y, y, s2); }
               }
-              sg[off >> 4] = s1;
-              qg[off >> 4] = s2;
+              sg[u][off >> 4] = s1;
+              qg[u][off >> 4] = s2;
             }
           }
+        }
         }
       }
     }
   }
-  if constexpr ((WTM == 32 || WTM == 64) && (BM / 64) * BN <= NT && (WTM / P) % 16 == 0) {
+  if constexpr ((WTM == 32 || WTM == 64) && (WTM / P) % 16 == 0) {
     if (st) {
-      const int b = tid / BN, j = tid - (tid / BN) * BN;
-      const int nn = n0 + j;
-      if (b < BM / 64 && nn < a.cout && rmap(b * 64) < a.M) {  // blocks past M are not in the buffer
-        float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + rmap(b * 64)) / 64) * a.cout + nn) * 2;
-        pp[0] = ((sg[0] + sg[1]) + sg[2]) + sg[3];
-        pp[1] = ((qg[0] + qg[1]) + qg[2]) + qg[3];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int b = (tid + u * NT) / BN, j = (tid + u * NT) % BN;
+        const int nn = n0 + j;
+        if (b < BM / 64 && nn < a.cout && rmap(b * 64) < a.M) {  // blocks past M are not in the buffer
+          float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + rmap(b * 64)) / 64) * a.cout + nn) * 2;
+          pp[0] = ((sg[u][0] + sg[u][1]) + sg[u][2]) + sg[u][3];
+          pp[1] = ((qg[u][0] + qg[u][1]) + qg[u][2]) + qg[u][3];
+        }
       }
       if (tid == 0 && rmap(0) == 0 && n0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
     }
@@ -286,7 +298,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
 template <int BM, int BN, int WGM, int NT, int P>
 constexpr bool stats_tile_ok() {
   constexpr int WTM = BM / WGM;
-  return (WTM == 32 || WTM == 64) && (WTM / P) % 16 == 0 && (BM / 64) * BN <= NT;
+  return (WTM == 32 || WTM == 64) && (WTM / P) % 16 == 0;
 }
 
 // GNP: compile the GroupNorm+SiLU gather prologue in (false = plain gather, fewer VGPRs / VALU).
@@ -832,6 +844,50 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)lds_dst, 16, (int)voff, soff, 0, 0);
 }
 
+// Per-element epilogue straight from the accumulators (tails, PixelShuffle stores, fp32 outputs
+// the vector epilogue does not take).
+template <int TM, int TN, int WTM, int WTN>
+__device__ __forceinline__ void epilogue_scalar(const f32x4 (&acc)[TM][TN], const ConvArgs& a, int m0, int n0, int wm,
+                                                int wn, int lane) {
+  if (a.out_mode == 2) return;  // unreachable: the host admits GEGLU only where the vector epilogue runs
+  const int lrow = lane & 15, lq = lane >> 4;
+  const int hw_o = a.ho * a.wo;
+  const bool of32 = a.out_f32;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
+      if (m >= a.M) continue;
+      const int img = m / hw_o;
+      int oy = 0, ox = 0;
+      if (a.out_mode == 1) { const int rem = m - img * hw_o; oy = rem / a.wo; ox = rem - oy * a.wo; }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nn = n0 + wn * WTN + j * 16 + lrow;
+        if (nn >= a.cout) continue;
+        float v = acc[i][j][r];
+        if (a.bias) v += a.bias[nn];
+        if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
+        v = apply_act(v, a.act, a.act_param);
+        long oidx, ridx;
+        if (a.out_mode == 1) {
+          const int c = nn >> 2, dy = (nn >> 1) & 1, dx = nn & 1;
+          const long p = ((long)img * (2 * a.ho) + (2 * oy + dy)) * (2 * a.wo) + (2 * ox + dx);
+          oidx = p * a.out_ld + c;
+          ridx = p * a.res_ld + c;
+        } else {
+          oidx = (long)m * a.out_ld + nn;
+          ridx = (long)m * a.res_ld + nn;
+        }
+        if (a.res) v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const bf16*>(a.res)[ridx]);
+        if (of32) reinterpret_cast<float*>(a.out)[oidx] = v;
+        else reinterpret_cast<bf16*>(a.out)[oidx] = from_f32<bf16>(v);
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int WGM, int WGN, int S, int EP>
 __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1,
                                               unsigned bytesw) {
@@ -998,41 +1054,7 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
       return;
     }
   }
-  if (a.out_mode == 2) return;  // unreachable: the host admits GEGLU only where the vector epilogue runs
-  const bool of32 = a.out_f32;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
-      if (m >= a.M) continue;
-      const int img = m / hw_o;
-      int oy = 0, ox = 0;
-      if (a.out_mode == 1) { const int rem = m - img * hw_o; oy = rem / a.wo; ox = rem - oy * a.wo; }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nn = n0 + wn * WTN + j * 16 + lrow;
-        if (nn >= a.cout) continue;
-        float v = acc[i][j][r];
-        if (a.bias) v += a.bias[nn];
-        if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
-        v = apply_act(v, a.act, a.act_param);
-        long oidx, ridx;
-        if (a.out_mode == 1) {
-          const int c = nn >> 2, dy = (nn >> 1) & 1, dx = nn & 1;
-          const long p = ((long)img * (2 * a.ho) + (2 * oy + dy)) * (2 * a.wo) + (2 * ox + dx);
-          oidx = p * a.out_ld + c;
-          ridx = p * a.res_ld + c;
-        } else {
-          oidx = (long)m * a.out_ld + nn;
-          ridx = (long)m * a.res_ld + nn;
-        }
-        if (a.res) v += of32 ? reinterpret_cast<const float*>(a.res)[ridx] : to_f32(reinterpret_cast<const bf16*>(a.res)[ridx]);
-        if (of32) reinterpret_cast<float*>(a.out)[oidx] = v;
-        else reinterpret_cast<bf16*>(a.out)[oidx] = from_f32<bf16>(v);
-      }
-    }
-  }
+  epilogue_scalar<TM, TN, WTM, WTN>(acc, a, m0, n0, wm, wn, lane);
 }
 
 // Kernel entry points. Residency: 1024-thread blocks need <= 80 SGPRs for two blocks per CU (the
