@@ -210,7 +210,10 @@ int rdeic_cast(const void* in, int32_t in_dtype, void* out, int32_t out_dtype, i
  * params: [pix][pld] with scales at channel 0..c-1 and means at c..2c-1 (chunk(2,1)).
  * Encode: y -> symbols/indexes written per image at sym + img*img_stride + off + (ch*hy + r)*(wy/2) + j
  * and yhat (= sym + mean) scattered to yhat[pix][yld] (+ anchor-only copy when anchor_out != NULL).
- * scale_table: the 64 GaussianConditional levels; lower bound 0.11 (compressai default). */
+ * scale_table: the 64 GaussianConditional levels; lower bound 0.11 (compressai default).
+ * sym / idx (and rdeic_ckbd_indexes' idx, rdeic_ckbd_dequant's sym) may be device memory or pinned
+ * host memory (hipHostMalloc / torch pin_memory: device-addressable), so the coder round trips need
+ * no copy launches; the caller orders host access with an event after the kernel. */
 int rdeic_ckbd_encode(const void* y, int32_t yld, const void* params, int32_t pld, int32_t n, int32_t hy,
                       int32_t wy, int32_t c, int32_t phase, const float* scale_table, int32_t levels,
                       float scale_bound, int32_t* sym, int32_t* idx, int64_t img_stride, int64_t off,

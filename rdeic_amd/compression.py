@@ -312,8 +312,9 @@ class Compression:
         def group(gi: int, b0: int, b1: int):
             nb = b1 - b0
             yg = y[b0:b1]
-            sym = torch.empty((nb, total), dtype=torch.int32, device=h.device)
-            idx = torch.empty((nb, total), dtype=torch.int32, device=h.device)
+            # the symbols and indexes go straight from the stage kernels into pinned host memory
+            # (device-addressable; ordered for the host by the event after the last stage): no copy
+            # launches on the stream
             sym_p = self._pinned(f"enc_sym{gi}", nb * total).view(nb, total)
             idx_p = self._pinned(f"enc_idx{gi}", nb * total).view(nb, total)
             done = torch.cuda.Event()
@@ -322,16 +323,14 @@ class Compression:
                 s0 = self.slice_off[i]
                 ys = yg[..., s0:s0 + c]
                 ops.call("rdeic_ckbd_encode", ys.data_ptr(), ops.pix_ld(ys), params.data_ptr(), ops.pix_ld(params), nb,
-                         hy, wy, c, phase, table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), sym.data_ptr(),
-                         idx.data_ptr(), total, off, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
+                         hy, wy, c, phase, table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), sym_p.data_ptr(),
+                         idx_p.data_ptr(), total, off, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
                          None if anchor is None else anchor.data_ptr(), 0 if anchor is None else ops.pix_ld(anchor),
                          dtc, ops.stream_ptr())
 
             yield from self._stage_gen(hyper[b0:b1], hy, wy, emit, [t[b0:b1] for t in bufs])
 
             def to_host():
-                sym_p.copy_(sym, non_blocking=True)
-                idx_p.copy_(idx, non_blocking=True)
                 done.record()
 
             host_step(to_host)
@@ -391,21 +390,21 @@ class Compression:
             nb = b1 - b0
             idx_pin = self._pinned(f"dec_idx{gi}", nb * nmax)  # sized once: no regrowth mid-loop
             sym_pin = self._pinned(f"dec_sym{gi}", nb * nmax)
-            sym_dev = torch.empty(nb * nmax, dtype=torch.int32, device=dev)
 
             def emit(i, phase, params, c, off, yhat_slice, anchor):
+                # the indexes kernel writes pinned host memory and the dequant kernel reads the decoded
+                # symbols from it (device-addressable): the round trip has no copy launches. The host
+                # reads after the event; it rewrites the symbols only after the next stage's event,
+                # which the stream orders after this stage's dequant.
                 n = c * hy * (wy // 2)
-                idx = torch.empty((nb, n), dtype=torch.int32, device=dev)
-                ops.call("rdeic_ckbd_indexes", params.data_ptr(), ops.pix_ld(params), nb, hy, wy, c, phase,
-                         table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), idx.data_ptr(), n, 0, dtc,
-                         ops.stream_ptr())
                 idx_p = idx_pin[:nb * n].view(nb, n)
                 sym_p = sym_pin[:nb * n].view(nb, n)
-                sym = sym_dev[:nb * n].view(nb, n)
+                ops.call("rdeic_ckbd_indexes", params.data_ptr(), ops.pix_ld(params), nb, hy, wy, c, phase,
+                         table.data_ptr(), table.numel(), float(coders.SCALE_BOUND), idx_p.data_ptr(), n, 0, dtc,
+                         ops.stream_ptr())
                 ready = torch.cuda.Event()
 
                 def to_host():
-                    idx_p.copy_(idx, non_blocking=True)
                     ready.record()
 
                 host_step(to_host)
@@ -414,10 +413,9 @@ class Compression:
                 def decode():
                     ready.synchronize()
                     coders.rans_decode_batch(self._io["decs"][b0:b1], idx_p.numpy(), self.tables, out=sym_p.numpy())
-                    sym.copy_(sym_p, non_blocking=True)
 
                 host_step(decode)
-                ops.call("rdeic_ckbd_dequant", sym.data_ptr(), params.data_ptr(), ops.pix_ld(params), nb, hy, wy, c,
+                ops.call("rdeic_ckbd_dequant", sym_p.data_ptr(), params.data_ptr(), ops.pix_ld(params), nb, hy, wy, c,
                          phase, n, 0, yhat_slice.data_ptr(), ops.pix_ld(yhat_slice),
                          None if anchor is None else anchor.data_ptr(), 0 if anchor is None else ops.pix_ld(anchor),
                          dtc, ops.stream_ptr())
