@@ -87,7 +87,8 @@ int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
  * concat segments multiples of 64 channels; other shapes fall back to the register path):
  * 20 256x256/8, 21 256x128/8, 22 128x256/8, 23-24 128x128/4, 25 128x128/8, 26 64x128/4,
  * 27 128x128/8, 28 256x128/8, 29 128x256/8, 30 64x128/4, 31 128x64/4, 32 256x256/16,
- * 33 256x128/16, 34 128x128/16, 35 512x128/16, 36 64x128/8 (ring depths in conv_gemm.hip). -1 = heuristic. All tiles give
+ * 33 256x128/16, 34 128x128/16, 35 512x128/16, 36 64x128/8, 37 128x160/4, 38 64x160/4 (ring depths in
+ * conv_gemm.hip). -1 = heuristic. All tiles give
  * bit-identical results (same k order, same MFMA), so a caller may autotune. */
 int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream);
 /* Split-K variant for small-M / large-K layers (the UNet's 8x8 and 16x16 levels): `splits`

@@ -1127,7 +1127,8 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
 //   25 128x128/8 S2, 26 64x128/4 S3, 27 128x128/8 S3, 28 256x128/8 S2, 29 128x256/8 S2,
 //   30 64x128/4 S2, 31 128x64/4 S2, 32 256x256/16 S2, 33 256x128/16 S2, 34 128x128/16 S2,
 //   35 512x128/16 S2 (64x64 per wave at cout = 128: the whole 160 KB of LDS, one block per CU),
-//   36 64x128/8 S2 (32x32 per wave: twice the waves of tile 30 on grids of ~256 tiles)
+//   36 64x128/8 S2 (32x32 per wave: twice the waves of tile 30 on grids of ~256 tiles),
+//   37 128x160/4 S2 and 38 64x160/4 S2 (N = 320 layers: two N tiles, no padded columns)
 // Measured (tools/dma_bench.py, one MI355X): 32 is best where a 256x256 grid fills the chip
 // without padding waste (1.19-1.27 PF on the VAE 512-channel layers), 25 on the rest with >= 256
 // 128x128 tiles, the 4-wave 64x128 tile when even that grid cannot fill the chip; 34 often wins
@@ -1135,7 +1136,7 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
 // tools/tune_tiles.py; shapes missing from it use this heuristic).
 int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int tile,
                     int gn_hw = 0, bool* fused = nullptr) {
-  if (tile < 20 || tile > 36) {
+  if (tile < 20 || tile > 38) {
     const long zb = a.splits > 1 ? a.splits : a.batch;
     const long t128 = (long)cdiv(a.M, 128) * cdiv(a.cout, 128) * zb;
     const long t256 = (long)cdiv(a.M, 256) * cdiv(a.cout, 256) * zb;
@@ -1159,6 +1160,8 @@ int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hi
     case 34: return launch_dma<128, 128, 4, 4, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
     case 35: return launch_dma<512, 128, 8, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
     case 36: return launch_dma<64, 128, 2, 4, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 37: return launch_dma<128, 160, 2, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 38: return launch_dma<64, 160, 2, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
     default: return launch_dma<128, 128, 2, 2, 3, 2>(a, b0, b1, bw, s, gn_hw, fused);
   }
 }

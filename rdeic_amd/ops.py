@@ -240,8 +240,8 @@ AUTOTUNE = False
 FORCE_TILE: Optional[int] = None  # tests / tools: run every eligible conv on this tile id
 GEGLU_FUSED = True  # bf16 transformer FF: GEGLU in the projection's epilogue (conv out_mode 2)
 TILE_CANDIDATES = (0, 1, 3, 4, 6, 8, 10)
-DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31, 35, 36)
-ALL_TILES = (0, 1, 2, 3, 4, 6, 7, 8, 9, 10) + tuple(range(20, 37))
+DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31, 35, 36, 37, 38)
+ALL_TILES = (0, 1, 2, 3, 4, 6, 7, 8, 9, 10) + tuple(range(20, 39))
 TILE_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tiles.json")
 
 

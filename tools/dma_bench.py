@@ -29,6 +29,10 @@ SHAPES = [
     ("unet1280@8", 16, 8, 8, 1280, 0, 1280, 3, 1, 0, None),
     ("unet_cat640+320@64", 16, 64, 64, 640, 320, 320, 3, 1, 0, None),
     ("unet_cat1280+1280@8", 16, 8, 8, 1280, 1280, 1280, 3, 1, 0, None),
+    ("unet640to320@64", 16, 64, 64, 640, 0, 320, 3, 1, 0, None),
+    ("unet960to320@64", 16, 64, 64, 960, 0, 320, 3, 1, 0, None),
+    ("lin1280x320", 1, 65536, 1, 1280, 0, 320, 1, 1, 0, None),
+    ("lin320x960", 1, 65536, 1, 320, 0, 960, 1, 1, 0, None),
     ("lin320x2560", 1, 65536, 1, 320, 0, 2560, 1, 1, 0, None),
     ("lin320x320", 1, 65536, 1, 320, 0, 320, 1, 1, 0, None),
     ("lin1280x1280", 1, 4096, 1, 1280, 0, 1280, 1, 1, 0, None),
@@ -43,7 +47,7 @@ SHAPES = [
     ("unet_cat640+320@32_1x1", 16, 32, 32, 640, 320, 640, 1, 1, 0, None),
     ("unet_cat1280+640@32_1x1", 16, 32, 32, 1280, 640, 640, 1, 1, 0, None),
 ]
-TILES = (-1, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36)
+TILES = (-1, 20, 21, 22, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38)
 
 
 def bench(fn, reps):
@@ -64,7 +68,7 @@ def main():
     tiles = [int(t) for t in args.tiles.split(",")]
     torch.manual_seed(0)
     for name, B, H, W, c0, c1, cout, k, stride, up2, padtl in SHAPES:
-        if args.only and args.only not in name:
+        if args.only and not any(o in name for o in args.only.split(",")):
             continue
         x = torch.randn(B, H, W, c0, device="cuda").to(torch.bfloat16)
         x2 = torch.randn(B, H, W, c1, device="cuda").to(torch.bfloat16) if c1 else None
