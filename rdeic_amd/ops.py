@@ -242,7 +242,9 @@ GEGLU_FUSED = True  # bf16 transformer FF: GEGLU in the projection's epilogue (c
 TILE_CANDIDATES = (0, 1, 3, 4, 6, 8, 10)
 DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31, 35, 36, 37, 38)
 ALL_TILES = (0, 1, 2, 3, 4, 6, 7, 8, 9, 10) + tuple(range(20, 39))
-TILE_TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tiles.json")
+# RDEIC_TILE_TABLE: another table file (same-box A/B of tile tables, tools/table_ab.sh)
+TILE_TABLE_PATH = os.environ.get("RDEIC_TILE_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                     "conv_tiles.json")
 
 
 def tile_key(m: int, c0: int, c1: int, p: "ConvParams", up2: bool, out_mode: int, res: bool, emb: bool, act: int,

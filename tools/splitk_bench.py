@@ -14,7 +14,9 @@ SHAPES = [("unet640@32", 16, 32, 32, 640, 640, (2, 3, 4, 6)), ("unet1280@16", 16
           ("unet1280@8", 16, 8, 8, 1280, 1280, (3, 4, 5, 6, 7, 8)), ("unet2560@8", 16, 8, 8, 2560, 1280, (4, 6, 7, 8)),
           # the entropy model's nets at y = 32x32 (512^2 images): 5x5 context / parameter convs, 3x3 g_s
           ("ep5x5 256->128@32", 16, 32, 32, 256, 128, (2, 3, 4, 6), 5), ("ep5x5 192->256@32", 16, 32, 32, 192, 256, (2, 3, 4), 5),
-          ("gs3x3 256->256@32", 16, 32, 32, 256, 256, (2, 3, 4)), ("c3x3 256->256@16", 16, 16, 16, 256, 256, (2, 3, 4, 6))]
+          ("gs3x3 256->256@32", 16, 32, 32, 256, 256, (2, 3, 4)), ("c3x3 256->256@16", 16, 16, 16, 256, 256, (2, 3, 4, 6, 9)),
+          # control net (0.2 x the UNet widths) at its 8x8 level: 16 tiles of 128x128 at B=16
+          ("c3x3 256->256@8", 16, 8, 8, 256, 256, (2, 3, 4, 6, 9, 12))]
 
 
 def timeit(fn, reps=10):
