@@ -18,6 +18,7 @@
 #include "prof.h"
 
 int rdeic_g_attn64 = 2;  // rdeic_set_conv_option(1, v): dh=64 kernel: 2 LDS-DMA (default), 1 register-staged, 0 generic
+int rdeic_g_attn512 = 2;  // rdeic_set_conv_option(8, v): d=512 kernel: 2 wave pairs (default), 1 one wave per 16 queries
 
 namespace {
 
@@ -1036,6 +1037,214 @@ __global__ __launch_bounds__(256) void attn512_kernel(const bf16* __restrict__ q
   }
 }
 
+// ============================================================================================
+// d = 512, wave-pair form (r03): attn512_kernel reads a whole 32-key K and V tile (64 KB) per wave
+// for only 16 queries, so its LDS bytes per MFMA equal the pipe's rate at one wave per SIMD. Here 8
+// waves = 4 pairs x 32 queries (128 per block): the two waves of a pair split d in halves. Each
+// computes the partial S^T of its 32 queries over its 256 d (its half of the K tile, 8 d-slices x 2
+// key blocks x 2 query groups = 32 MFMAs), the pair exchanges the partials through LDS (4 KB per
+// wave, one barrier) and both form S = S_lo + S_hi (fp32 addition commutes: the two waves hold
+// identical scores), run the same online softmax, and accumulate O^T for their own 256 d (half of
+// the V^T reads, 16 d-blocks x 2 query groups). Per MFMA this is half the K/V LDS traffic, at two
+// waves per SIMD (≈190 VGPRs: O^T 128, Q^T 64). LDS: the 2 x 64 KB K/V ring + 32 KB exchange.
+// Summation order per output: the same k (key) order as attn512_kernel, but S is now the sum of
+// two 256-d partials: results differ from attn512_kernel by fp32 rounding (deterministic).
+// ============================================================================================
+constexpr int A512P_Q = 128, A512P_X = 8 * 4096;
+
+__global__ __launch_bounds__(512) void attn512p_kernel(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
+                                                       int ldk, const bf16* __restrict__ v, int ldv,
+                                                       bf16* __restrict__ o, int ldo, int lq, int lk, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // 2 x (K tile | V tile), then exchange
+  char* const xbuf = lds + 2 * A512_STAGE;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pr = wave & 3, hf = wave >> 2;  // query group of the pair, d half
+  const int lr = lane & 15, g = lane >> 4;
+  const bf16* qb = q + (long)b * lq * ldq;
+  const bf16* kb = k + (long)b * lk * ldk;
+  const bf16* vb = v + (long)b * lk * ldv;
+  const int q0 = blockIdx.x * A512P_Q + pr * 32;
+
+  // Q^T fragments of this wave's d half: [query group u][d slice hd]: d = 32 (8 hf + hd) + 8g
+  bf16x8 qf[2][8];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int qq = q0 + 16 * u + lr;
+    const bf16* qr = qb + (long)min(qq, lq - 1) * ldq + 256 * hf + 8 * g;
+#pragma unroll
+    for (int hd = 0; hd < 8; ++hd) {
+      bf16x8 z = *reinterpret_cast<const bf16x8*>(qr + 32 * hd);
+      if (qq >= lq) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
+      }
+      qf[u][hd] = z;
+    }
+  }
+
+  const __amdgpu_buffer_rsrc_t rsk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)kb, (short)0, (int)(((long)(lk - 1) * ldk + 512) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)vb, (short)0, (int)(((long)(lk - 1) * ldv + 512) * 2), 0x00020000);
+  // DMA: wave w fills K rows 4w..4w+3 and V rows 4w..4w+3 (one 1 KB row per wave-instruction);
+  // the source offsets are recomputed at each issue from a laundered lane (no registers held)
+  auto issue = [&](int kt, int slot) {
+    char* sb = lds + slot * A512_STAGE;
+    int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));  // lane id, recomputed
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 4 * wave + j;
+      const unsigned key = (unsigned)(kt * A512_KT + row);
+      const unsigned kc = (unsigned)(ln ^ (row & 15)), vc = (unsigned)(ln ^ ((row & 7) << 1));
+      attn_dma16(rsk, sb + row * 1024, key * (unsigned)(ldk * 2) + kc * 16u);
+      attn_dma16(rsv, sb + A512_TILE + row * 1024, key * (unsigned)(ldv * 2) + vc * 16u);
+    }
+  };
+  // K fragment rows lr / 16 + lr, chunk (4 sd + g) ^ lr: with sd = 4 a + c the chunk is
+  // 4 a + ((4 c + g) ^ lr) (lr < 16), so four per-lane offsets (c = 0..3) and immediates serve all
+  // slices. V^T block 2 (16 hf + dt) + (vp >> 1), dt = 8 a + c, XORed with an even swz < 16:
+  // 32 hf + 16 a + ((2 c + (vp >> 1)) ^ swz), eight per-lane offsets (c = 0..7).
+  unsigned koff[4], voff[8];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) koff[c] = (unsigned)(lr * 1024 + (((4 * c + g) ^ lr) * 16));
+  const int row0 = 4 * g + (lr >> 2);
+  const int swz = (row0 & 7) << 1;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) voff[c] = (unsigned)(row0 * 1024 + ((lr & 3) & 1) * 8 + (((2 * c + ((lr & 3) >> 1)) ^ swz) * 16));
+
+  f32x4 oacc[2][16];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < 16; ++dt) oacc[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-INFINITY, -INFINITY};
+  float lsum[2] = {0.f, 0.f};
+  float* const xown = reinterpret_cast<float*>(xbuf + wave * 4096) + lane * 16;
+  const float* const xpar = reinterpret_cast<const float*>(xbuf + (wave ^ 4) * 4096) + lane * 16;
+
+  const int ntiles = lk / A512_KT;
+  issue(0, 0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    attn_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // this tile landed; every read of the other slot (and of the
+                                   // exchange buffer, one tile back) is done
+    if (kt + 1 < ntiles) issue(kt + 1, (kt + 1) & 1);
+    const char* Kt = lds + (kt & 1) * A512_STAGE;
+    const char* Vt = Kt + A512_TILE;
+    f32x4 st[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) st[u][0] = st[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* Kh = Kt + hf * 512;  // slices 8 hf .. 8 hf + 7: a = 2 hf + (hd >> 2)
+#pragma unroll
+    for (int hd = 0; hd < 8; ++hd) {
+      if (hd % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // K fragments in flight: 4 slices (VGPR budget)
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(Kh + koff[hd & 3] + (hd >> 2) * 256);
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(Kh + koff[hd & 3] + (hd >> 2) * 256 + 16 * 1024);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        st[u][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[u][hd], st[u][0], 0, 0, 0);
+        st[u][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[u][hd], st[u][1], 0, 0, 0);
+      }
+    }
+    // pair exchange of the partial scores (lane-for-lane identical layout in both waves)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int kb2 = 0; kb2 < 2; ++kb2) *reinterpret_cast<f32x4*>(xown + 8 * u + 4 * kb2) = st[u][kb2];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int kb2 = 0; kb2 < 2; ++kb2) st[u][kb2] += *reinterpret_cast<const f32x4*>(xpar + 8 * u + 4 * kb2);
+
+    bf16x8 pf[2];
+    bool rescale = false;
+    float alpha[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float mx = st[u][0][0];
+#pragma unroll
+      for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[u][kb2][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float ms = mx * scale_log2;
+      alpha[u] = 1.f;
+      if (ms > m_run[u] + 8.f) {
+        alpha[u] = __builtin_amdgcn_exp2f(m_run[u] - ms);
+        m_run[u] = ms;
+        rescale = true;
+      }
+      const float nm = -m_run[u];
+      float ps = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pf[u][j] = (bf16)__builtin_amdgcn_exp2f(fmaf(st[u][j >> 2][j & 3], scale_log2, nm));
+        ps += (float)pf[u][j];
+      }
+      lsum[u] = lsum[u] * alpha[u] + ps;
+    }
+    if (__any(rescale)) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int dt = 0; dt < 16; ++dt) oacc[u][dt] *= alpha[u];
+    }
+    // O^T[u][dt] (16 d x 16 queries) += V^T (16 d x 32 keys) P^T[u] for this wave's 16 d-blocks
+    const unsigned vbase = (unsigned)(uintptr_t)(lds_vptr_t)Vt + hf * 512;
+    auto vaddr = [&](int dt) { return vbase + voff[dt & 7] + (dt >> 3) * 256; };
+    constexpr int VD = 3;  // V^T d-blocks in flight (VGPR budget at two waves per SIMD)
+    v4s vt[VD][2];
+#pragma unroll
+    for (int w = 0; w < VD - 1; ++w) {
+      vt[w][0] = ds_read_tr16_off<0>(vaddr(w));
+      vt[w][1] = ds_read_tr16_off<16 * 1024>(vaddr(w));
+    }
+#pragma unroll
+    for (int dt = 0; dt < 16; ++dt) {
+      const int cb = dt % VD;
+      if (dt + VD - 1 < 16) {
+        const unsigned a = vaddr(dt + VD - 1);
+        vt[(dt + VD - 1) % VD][0] = ds_read_tr16_off<0>(a);
+        vt[(dt + VD - 1) % VD][1] = ds_read_tr16_off<16 * 1024>(a);
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * (VD - 1)) : "memory");
+      } else if (dt + 1 < 16) {
+        asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      tie(vt[cb][0]);
+      tie(vt[cb][1]);
+      const v4s both[2] = {vt[cb][0], vt[cb][1]};
+      const bf16x8 vf = *reinterpret_cast<const bf16x8*>(both);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) oacc[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[u], oacc[u][dt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float l = lsum[u];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+    const int qq = q0 + 16 * u + lr;
+    if (qq < lq) {
+      bf16* orow = o + ((long)b * lq + qq) * ldo + 256 * hf;
+#pragma unroll
+      for (int dt = 0; dt < 16; ++dt) {
+        bf16x4 ov;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ov[i] = (bf16)(oacc[u][dt][i] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = ov;
+      }
+    }
+  }
+}
+
 template <typename T>
 int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo, int batch,
                 int heads, int lq, int lk, int dh, float scale, int kv_bcast, hipStream_t s) {
@@ -1044,6 +1253,13 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
       if (heads != 1 || kv_bcast || lk % A512_KT || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4 || ((uintptr_t)o) % 8 ||
           (long)(lk - 1) * (ldk > ldv ? ldk : ldv) * 2 + 1024 >= (1l << 31))
         return RDEIC_EINVAL;
+      // the wave-pair form needs >= 256 blocks of 128 queries; small grids keep the 64-query blocks
+      if (rdeic_g_attn512 == 2 && (long)((lq + A512P_Q - 1) / A512P_Q) * batch >= 256) {
+        dim3 grid((lq + A512P_Q - 1) / A512P_Q, batch);
+        hipLaunchKernelGGL(attn512p_kernel, grid, dim3(512), 2 * A512_STAGE + A512P_X, s, (const bf16*)q, ldq,
+                           (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f);
+        return launch_status();
+      }
       dim3 grid((lq + A512_Q - 1) / A512_Q, batch);
       hipLaunchKernelGGL(attn512_kernel, grid, dim3(256), 2 * A512_STAGE, s, (const bf16*)q, ldq, (const bf16*)k, ldk,
                          (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f);

@@ -1702,6 +1702,7 @@ extern "C" int rdeic_set_conv_path(int32_t path) {
 }
 
 extern int rdeic_g_attn64;
+extern int rdeic_g_attn512;
 
 extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 0) { int prev = g_epi_vec; g_epi_vec = value; return prev; }
@@ -1711,5 +1712,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 4) { int prev = g_force_tile; g_force_tile = value; return prev; }
   if (key == 5) { int prev = g_dma; g_dma = value; return prev; }
   if (key == 6) { int prev = g_halo; g_halo = value; return prev; }
+  if (key == 8) { int prev = rdeic_g_attn512; rdeic_g_attn512 = value; return prev; }
   return RDEIC_EINVAL;
 }
