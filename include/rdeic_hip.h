@@ -111,8 +111,9 @@ int rdeic_set_conv_path(int32_t path);
  * key 5: LDS-DMA conv kernel for 64-channel-aligned layers on (1, default) / off (0);
  * key 6: halo-strip 3x3 conv with the GroupNorm applied in LDS: 0 off, 1 GroupNorm-input convs
  *        (default), 2 every eligible conv (its k order differs from the im2col tiles');
- * key 8: head-dim-512 attention: 2 wave pairs splitting d over 32 queries (default, grids of >= 256
- *        128-query blocks), 1 one wave per 16 queries (fp32-rounding-level differences);
+ * key 8: head-dim-512 attention: 2 wave pairs splitting d over 32 queries (default, for L >= 4096:
+ *        a per-image rule, so outputs stay batch-invariant), 1 one wave per 16 queries everywhere
+ *        (fp32-rounding-level differences);
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way
  * (keys 0-5; 6 and 8 change fp32 rounding only). */
 int rdeic_set_conv_option(int32_t key, int32_t value);

@@ -1253,8 +1253,10 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
       if (heads != 1 || kv_bcast || lk % A512_KT || ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4 || ((uintptr_t)o) % 8 ||
           (long)(lk - 1) * (ldk > ldv ? ldk : ldv) * 2 + 1024 >= (1l << 31))
         return RDEIC_EINVAL;
-      // the wave-pair form needs >= 256 blocks of 128 queries; small grids keep the 64-query blocks
-      if (rdeic_g_attn512 == 2 && (long)((lq + A512P_Q - 1) / A512P_Q) * batch >= 256) {
+      // the form is a function of the per-image length only (never of the batch: the VAE encoder's
+      // output must not depend on how many images share a launch — the bitstreams are batch-invariant):
+      // wave pairs from 64^2 latents (L = 4096) up, the 64-query blocks below
+      if (rdeic_g_attn512 == 2 && lq >= 4096) {
         dim3 grid((lq + A512P_Q - 1) / A512P_Q, batch);
         hipLaunchKernelGGL(attn512p_kernel, grid, dim3(512), 2 * A512_STAGE + A512P_X, s, (const bf16*)q, ldq,
                            (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lq, lk, scale * 1.4426950408889634f);
