@@ -100,7 +100,8 @@ class GaussianTables:
 
 def default_threads() -> int:
     """Host coder threads per call: the CPUs this process can use (affinity set, capped by the
-    cgroup CPU quota: a GPU box shows 256 CPUs but grants 16), at most 16."""
+    cgroup CPU quota: a GPU box shows 256 CPUs but grants 16), shared among the ranks of this node
+    (LOCAL_WORLD_SIZE, set by torch.distributed.run: one process per GPU), at most 16."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -111,6 +112,10 @@ def default_threads() -> int:
         if quota != "max":
             n = min(n, max(1, int(quota) // int(period)))
     except (OSError, ValueError):
+        pass
+    try:
+        n //= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    except ValueError:
         pass
     return max(1, min(16, n))
 
