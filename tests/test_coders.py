@@ -218,3 +218,15 @@ def test_tabled_encoder_bytes_and_reciprocals(tables, gold):
             for x in xs:
                 assert lib.rdeic_rans_enc_quotient(h, row, v, x, C.byref(q)) == 0
                 assert q.value == x // f, (row, v, f, x)
+
+
+def test_default_threads_shared_among_local_ranks(monkeypatch):
+    """The host coder pool divides the CPU quota among the node's ranks (one process per GPU under
+    torch.distributed.run), so an 8-GPU node does not run 8 full-size pools per host."""
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    n1 = coders.default_threads()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    n4 = coders.default_threads()
+    assert 1 <= n4 <= n1 <= 16
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1000")
+    assert coders.default_threads() == 1
