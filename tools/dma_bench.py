@@ -41,6 +41,7 @@ SHAPES = [
     ("lin5120x1280", 1, 4096, 1, 5120, 0, 1280, 1, 1, 0, None),
     ("lin2560x640", 1, 16384, 1, 2560, 0, 640, 1, 1, 0, None),
     ("tail3x20x20_128to192", 3, 20, 20, 128, 0, 192, 3, 1, 0, None),
+    ("comp3x3_256to256@32", 16, 32, 32, 256, 0, 256, 3, 1, 0, None),
     ("comp5x5_256to128@32", 16, 32, 32, 256, 0, 128, 5, 1, 0, None),
     ("comp5x5_128to128@32", 16, 32, 32, 128, 0, 128, 5, 1, 0, None),
     ("comp3x3_256to384@32", 16, 32, 32, 256, 0, 384, 3, 1, 0, None),
