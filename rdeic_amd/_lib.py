@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "librdeic_hip.so")
+LIB_PATH = os.environ.get("RDEIC_LIB") or os.path.join(_HERE, "lib", "librdeic_hip.so")
 
 EINVAL, ENOSPC, EBADMSG, ELAUNCH = -22, -28, -74, -5
 _ERRNAMES = {EINVAL: "EINVAL (bad argument/shape)", ENOSPC: "ENOSPC (output capacity)",
