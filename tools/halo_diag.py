@@ -28,6 +28,8 @@ def main():
         ops.set_halo_conv(1)
         full = timeit(lambda: ops.conv2d(x, p, gn=ab, gn_silu=True, res=res, out=out, stats=True))
         gn_only = timeit(lambda: ops.conv2d(x, p, gn=ab, gn_silu=True, out=out))
+        gn_res = timeit(lambda: ops.conv2d(x, p, gn=ab, gn_silu=True, res=res, out=out))
+        gn_st = timeit(lambda: ops.conv2d(x, p, gn=ab, gn_silu=True, out=out, stats=True))
         ops.set_halo_conv(2)
         plain = timeit(lambda: ops.conv2d(x, p, out=out))
         plain_epi = timeit(lambda: ops.conv2d(x, p, res=res, out=out, stats=True))
@@ -37,7 +39,8 @@ def main():
         tf = lambda ms: flops / ms / 1e9  # noqa: E731
         print(f"{h}x{cin}x{cout}: full {full:.3f} ms ({tf(full):.0f} TF) | gn, no res/stats {gn_only:.3f} "
               f"({tf(gn_only):.0f}) | no gn {plain:.3f} ({tf(plain):.0f}) | no gn + res/stats {plain_epi:.3f} "
-              f"({tf(plain_epi):.0f}) | im2col tile, no gn {tile:.3f} ({tf(tile):.0f})", flush=True)
+              f"({tf(plain_epi):.0f}) | im2col tile, no gn {tile:.3f} ({tf(tile):.0f}) | gn + res only {gn_res:.3f} "
+              f"| gn + stats only {gn_st:.3f}", flush=True)
 
 
 if __name__ == "__main__":
