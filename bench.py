@@ -8,7 +8,8 @@ Data: synthetic (seeded smooth images, random-init weights of the real architect
 [1, 77, 1024] text context) — no datasets or checkpoints offline.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 16] [--size 512] [--ddim-steps 2]
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL).
+For N > 1 either run it as is (it starts N ranks itself: rdeic_amd/launch.py) or under
+torch.distributed.run with --nproc-per-node N (WORLD_SIZE must equal --gpus); one process per GPU, RCCL.
 """
 from __future__ import annotations
 
@@ -92,6 +93,9 @@ def parse():
 
 def main():
     args = parse()
+    # --gpus N > 1 without torch.distributed.run: this process only launches N ranks (never touches the GPU)
+    from rdeic_amd.launch import maybe_launch
+    maybe_launch(args.gpus, __file__)
     from rdeic_amd import metrics as quality, ops, parallel
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import relay_noise, synth_context, synth_image
@@ -291,7 +295,9 @@ def main():
                              "ms_per_step": round(kms / args.steps, 3)}
         roof["secondary"] = sec
     cpu = None
-    if not args.no_cpu_baseline:
+    if world > 1:
+        cpu = {"value": None, "note": "reported on rank 0 of the one-GPU run only (bench.py --gpus 1)"}
+    elif not args.no_cpu_baseline:
         log("cpu baseline (oracle restatement on the host cores)")
         try:
             from oracle.bench_cpu import run_cpu_baseline

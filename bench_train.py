@@ -8,7 +8,8 @@ One step = one batch of B synthetic 512x512 OOD-satellite-shaped images per GPU 
 with the reference's precision (fp32, finetune_ood.yaml `precision: 32`) by default.
 
   python bench_train.py [--gpus N] [--steps K] [--warmup W] [--batch 1] [--size 512] [--dtype fp32|bf16]
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL). Prints ONE JSON line.
+For N > 1 run it as is (it starts N ranks itself, rdeic_amd/launch.py) or under torch.distributed.run
+(WORLD_SIZE must equal --gpus); one process per GPU, RCCL. Prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -44,6 +45,8 @@ def parse(argv=None):
 
 def main(argv=None):
     args = parse(argv)
+    from rdeic_amd.launch import maybe_launch
+    maybe_launch(args.gpus, __file__, sys.argv[1:] if argv is None else list(argv))
     from rdeic_amd import ops, parallel
     from rdeic_amd.finetune import CapturedStep, FineTuner, nchw_draws_to_nhwc
     from rdeic_amd.rdeic import RDEIC

@@ -99,23 +99,30 @@ class GaussianTables:
 
 
 def default_threads() -> int:
-    """Host coder threads per call: the CPUs this process can use (affinity set, capped by the
-    cgroup CPU quota: a GPU box shows 256 CPUs but grants 16), shared among the ranks of this node
-    (LOCAL_WORLD_SIZE, set by torch.distributed.run: one process per GPU), at most 16."""
+    """Host coder threads per call, at most 16. RDEIC_CODER_THREADS overrides. Otherwise: the CPUs
+    this process may run on (affinity set), capped by the cgroup CPU quota (a GPU box shows 256 CPUs
+    but grants 16). The quota is shared by every rank of this node (LOCAL_WORLD_SIZE, one process
+    per GPU), so each rank takes quota / LWS; the affinity set is divided the same way only when it is
+    node-wide — a launcher that binds each rank to its own cores has already split it."""
+    env = os.environ.get("RDEIC_CODER_THREADS")
+    if env:
+        return max(1, int(env))
     try:
-        n = len(os.sched_getaffinity(0))
+        lws = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    except ValueError:
+        lws = 1
+    try:
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
+        aff = os.cpu_count() or 1
+    node = os.cpu_count() or aff
+    n = aff // lws if aff >= node else aff
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
             quota, period = f.read().split()[:2]
         if quota != "max":
-            n = min(n, max(1, int(quota) // int(period)))
+            n = min(n, max(1, int(quota) // int(period) // lws))
     except (OSError, ValueError):
-        pass
-    try:
-        n //= max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-    except ValueError:
         pass
     return max(1, min(16, n))
 

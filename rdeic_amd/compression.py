@@ -180,7 +180,7 @@ class Compression:
         if self._en is None or self._en.device != z.device:
             self._en = torch.empty(E.shape[0], dtype=torch.float32, device=z.device)
             ops.call("rdeic_row_sqnorm", E.data_ptr(), E.shape[0], N, N, self._en.data_ptr(), 0, ops.stream_ptr())
-        dot = ops.linear(zf, self.store.conv(self.p + "quantize.embedding", dtype=torch.float32))
+        dot = ops.linear(zf, self.store.conv(self.p + "quantize.embedding", dtype=torch.float32), images=B)
         idx = torch.empty(rows, dtype=torch.int32, device=z.device)
         ops.call("rdeic_vq_argmin", dot.data_ptr(), zn.data_ptr(), self._en.data_ptr(), rows, E.shape[0],
                  idx.data_ptr(), ops.stream_ptr())

@@ -54,7 +54,7 @@ class FineTuner:
         """embed_prob: the VectorQuantiser's codebook-usage EMA buffer
         (`preprocess_model.quantize.embed_prob` of a reference checkpoint or of train.py's own; zeros
         when absent, as a freshly built VectorQuantiser, compression_modules.py:239-241). It sets which
-        codes the next step re-initialises (decay = exp(-embed_prob * N * 10 / (1 - 0.99)) - 1e-3,
+        codes the next step re-initialises (decay = exp(-(embed_prob * N * 10) / (1 - 0.99) - 1e-3),
         compression_modules.py:272-296), so a resumed run must carry it."""
         self.m = model
         self.cfg = cfg or FineTuneConfig(used_timesteps=model.used_timesteps)

@@ -12,6 +12,7 @@ import ctypes as C
 import json
 import math
 import os
+import threading
 from dataclasses import dataclass
 from typing import Optional
 
@@ -292,16 +293,23 @@ def _autotune_tile(d0, scratch: torch.Tensor, candidates=None) -> int:
 
 
 # Split-K is opt-in (see splitk_allowed): it changes the k grouping, so layers whose outputs must
-# be batch-invariant (the entropy-model nets) never use it.
-SPLITK_ALLOWED = False
+# be batch-invariant (the entropy-model nets) never use it. The switches are PER HOST THREAD: codec
+# sessions run compress / decompress on their own threads, and one session leaving its split-K region
+# must not turn split-K off under another session's entropy nets (their encoder and decoder would then
+# compute different mu / sigma).
 _SPLITK_WS: dict = {}
+_SPLITK_TLS = threading.local()
 
 
-SPLITK_SHORT = False  # training: also split the short-K (k-tiles >= 8) small-M layers
+def splitk_state():
+    """(allowed, short_k) of the calling thread's split-K switches."""
+    return getattr(_SPLITK_TLS, "allowed", False), getattr(_SPLITK_TLS, "short", False)
+
+
 # Inference picks the split count from the layer's PER-IMAGE shape, as if the batch were
 # SPLITK_NOMINAL_BATCH images (config 2's 16): the k grouping of every output element then does not
 # depend on how many images share the launch, so one bitstream decodes to the same pixels in any
-# batch (bench, CLI --batch_size / --micro_batch_size, data-parallel shards). Training (SPLITK_SHORT,
+# batch (bench, CLI --batch_size / --micro_batch_size, data-parallel shards). Training (short_k,
 # B=1) sizes splits from the real M: it needs no batch invariance.
 SPLITK_NOMINAL_BATCH = 16
 # bf16 entropy model (Compression nets at the y / z resolution): split-K allowed, per-image counts
@@ -309,28 +317,28 @@ SPLITK_ENTROPY = True
 
 
 class splitk_allowed:
-    """Context manager enabling split-K for small-M / large-K convs (UNet / control forward).
-    short_k (the fine-tune step, B=1): also split layers with as few as 8 k-tiles."""
+    """Context manager enabling split-K for small-M / large-K convs (UNet / control forward) on the
+    calling thread. short_k (the fine-tune step, B=1): also split layers with as few as 8 k-tiles."""
 
     def __init__(self, short_k: bool = False):
         self.short_k = short_k
 
     def __enter__(self):
-        global SPLITK_ALLOWED, SPLITK_SHORT
-        self._prev = (SPLITK_ALLOWED, SPLITK_SHORT)
-        SPLITK_ALLOWED, SPLITK_SHORT = True, self.short_k or SPLITK_SHORT
+        self._prev = splitk_state()
+        _SPLITK_TLS.allowed, _SPLITK_TLS.short = True, self.short_k or self._prev[1]
+        return self
 
     def __exit__(self, *exc):
-        global SPLITK_ALLOWED, SPLITK_SHORT
-        SPLITK_ALLOWED, SPLITK_SHORT = self._prev
+        _SPLITK_TLS.allowed, _SPLITK_TLS.short = self._prev
 
 
-def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor, n: int = 1) -> int:
+def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor, n: int) -> int:
     """Number of k-splits (1 = none): only when the 128x128 tile grid cannot fill the chip.
-    Inference: a function of the per-image M only (SPLITK_NOMINAL_BATCH)."""
-    if not SPLITK_SHORT:
+    Inference: a function of the per-image M only (SPLITK_NOMINAL_BATCH); n = images in the launch."""
+    allowed, short = splitk_state()
+    if not short:
         M = (M // max(1, n)) * SPLITK_NOMINAL_BATCH
-    if not SPLITK_ALLOWED or fused or x.dtype not in (torch.bfloat16, torch.float32) or p.cout % 8 \
+    if not allowed or fused or x.dtype not in (torch.bfloat16, torch.float32) or p.cout % 8 \
             or pix_ld(out) % 8 or out.data_ptr() % 16:
         return 1
     for t in (x, x2):
@@ -339,14 +347,14 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
     if x.dtype == torch.float32:  # 64x64 fp32 tiles, 32-deep k-steps
         tiles = -(-M // 64) * -(-p.cout // 64)
         nk = -(-(p.kh * p.kw * p.cin) // 32)
-        if SPLITK_SHORT and tiles < 256 and 8 <= nk < 32:
+        if short and tiles < 256 and 8 <= nk < 32:
             return max(1, min(-(-512 // tiles), nk // 4, 16))
         if tiles >= 256 or nk < 32:
             return 1
         return max(1, min(-(-512 // tiles), nk // 8, 16))
     tiles = -(-M // 128) * -(-p.cout // 128)
     nk = -(-(p.kh * p.kw * p.cin) // 64)
-    if SPLITK_SHORT and tiles < 128 and 8 <= nk < 32:
+    if short and tiles < 128 and 8 <= nk < 32:
         return max(1, min(-(-512 // tiles), nk // 4, 8))
     if tiles >= 192 or nk < 32:
         return 1
@@ -529,9 +537,10 @@ def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) 
 
 def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, geglu: bool = False,
-           stats_hw: Optional[int] = None, images: int = 1) -> torch.Tensor:
+           stats_hw: Optional[int] = None, images: int) -> torch.Tensor:
     """Token-wise Linear over a [rows, c] tensor (1x1 conv over a rows x 1 image).
-    images: the number of images whose tokens the rows hold (the per-image split-K choice).
+    images: the number of images whose tokens the rows hold (required: the per-image split-K choice
+    keeps every output's k grouping independent of the batch).
     geglu: fused GEGLU projection (p from ParamStore.conv_geglu), output [rows, cout/2].
     stats_hw: the output (as [rows/stats_hw images, stats_hw tokens]) feeds a GroupNorm; its
     statistics are produced with it (conv2d(stats=True)); reshape with ops.tokens_to_nhwc."""

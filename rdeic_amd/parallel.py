@@ -20,8 +20,8 @@ def init_from_env(backend: str = None) -> Tuple[int, int, int]:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # RDEIC_DIST_BACKEND=gloo: launcher rehearsals with several ranks on one GPU
+            backend = os.environ.get("RDEIC_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -35,6 +35,10 @@ def shard(global_batch: int, rank: int, world: int) -> Tuple[int, int]:
     base, rem = divmod(global_batch, world)
     start = rank * base + min(rank, rem)
     return start, start + base + (1 if rank < rem else 0)
+
+
+def _gloo() -> bool:
+    return dist.get_backend() == "gloo"
 
 
 def gather_metrics(rows: torch.Tensor, global_batch: int = None) -> torch.Tensor:
@@ -51,18 +55,21 @@ def gather_metrics(rows: torch.Tensor, global_batch: int = None) -> torch.Tensor
     if rows.shape[0] != sizes[rank][1] - sizes[rank][0]:
         raise ValueError(f"rank {rank} holds {rows.shape[0]} rows, its shard of {global_batch} is {sizes[rank]}")
     bmax = max(e - s for s, e in sizes)
+    dev = rows.device
+    if _gloo():  # gloo collectives on host tensors (RCCL takes the device tensor as is)
+        rows = rows.cpu()
     send = rows.new_zeros((bmax, rows.shape[1]))
     send[: rows.shape[0]] = rows
     out = torch.empty((world * bmax, rows.shape[1]), dtype=rows.dtype, device=rows.device)
     dist.all_gather_into_tensor(out, send)
     out = out.view(world, bmax, rows.shape[1])
-    return torch.cat([out[r, : e - s] for r, (s, e) in enumerate(sizes)])
+    return torch.cat([out[r, : e - s] for r, (s, e) in enumerate(sizes)]).to(dev)
 
 
 def max_over_ranks(value: float, device) -> float:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device="cpu" if _gloo() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -75,7 +82,7 @@ def finish() -> None:
 
 def barrier(device=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and not _gloo():
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

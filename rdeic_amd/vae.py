@@ -117,7 +117,8 @@ class AutoencoderKL:
         else:  # fp32 parity mode: the materialised GEMM -> softmax -> GEMM (reference op order)
             ops.attention_single_head_materialized(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch=B,
                                                    length=L, dim=C, scale=int(C) ** (-0.5))
-        out = ops.linear(o, s.conv(pre + ".proj_out"), res=x.contiguous().view(B * L, C), stats_hw=L)
+        out = ops.linear(o, s.conv(pre + ".proj_out"), res=x.contiguous().view(B * L, C), stats_hw=L,
+                          images=B)
         return ops.tokens_to_nhwc(out, B, H, W_)
 
     # ------------------------------------------------------------------ passes

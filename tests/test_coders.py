@@ -230,3 +230,26 @@ def test_default_threads_shared_among_local_ranks(monkeypatch):
     assert 1 <= n4 <= n1 <= 16
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1000")
     assert coders.default_threads() == 1
+
+
+def test_default_threads_respects_per_rank_binding(monkeypatch):
+    """A launcher that binds each rank to its own cores has already split the CPUs: the affinity set is
+    not divided again, and RDEIC_CODER_THREADS overrides everything."""
+    import os
+    monkeypatch.delenv("RDEIC_CODER_THREADS", raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setattr(os, "cpu_count", lambda: 64)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(6)), raising=False)
+    import builtins
+    real_open = builtins.open
+
+    def no_quota(path, *a, **k):
+        if str(path) == "/sys/fs/cgroup/cpu.max":
+            raise OSError("no cgroup")
+        return real_open(path, *a, **k)
+    monkeypatch.setattr(builtins, "open", no_quota)
+    assert coders.default_threads() == 6          # bound per rank: 6 own cores, not 6 // 8
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)), raising=False)
+    assert coders.default_threads() == 8          # node-wide affinity: 64 // 8
+    monkeypatch.setenv("RDEIC_CODER_THREADS", "3")
+    assert coders.default_threads() == 3

@@ -80,7 +80,7 @@ def test_fused_stats_concat_linear_and_splitk(gpu):
     B, H, W, C = 2, 32, 32, 640
     t_in = torch.randn(B * H * W, C, device="cuda").to(torch.bfloat16)
     r = torch.randn(B * H * W, C, device="cuda").to(torch.bfloat16)
-    out = ops.tokens_to_nhwc(ops.linear(t_in, _conv(C, C, k=1, seed=4), res=r, stats_hw=H * W), B, H, W)
+    out = ops.tokens_to_nhwc(ops.linear(t_in, _conv(C, C, k=1, seed=4), res=r, stats_hw=H * W, images=B), B, H, W)
     gamma, beta = _gamma_beta(C)
     ab_f = ops.group_norm_ab(out, gamma, beta, 32, 1e-6)
     torch.testing.assert_close(ab_f, _standalone(out, gamma, beta, 32, 1e-6), rtol=2e-4, atol=2e-5)

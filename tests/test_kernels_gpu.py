@@ -323,8 +323,8 @@ def test_linear_fused_geglu(gpu, rows, cin, inner):
     st.shapes["ff.weight"], st.shapes["ff.bias"] = tuple(w.shape), tuple(b.shape)
     st.t["ff.weight"], st.t["ff.bias"] = w.cuda(), b.cuda()
     xb = x.to(torch.bfloat16).cuda()
-    fused = ops.linear(xb, st.conv_geglu("ff"), geglu=True)
-    unfused = ops.geglu(ops.linear(xb, st.conv("ff")))
+    fused = ops.linear(xb, st.conv_geglu("ff"), geglu=True, images=1)
+    unfused = ops.geglu(ops.linear(xb, st.conv("ff"), images=1))
     assert fused.shape == (rows, inner)
     assert (fused.float() - unfused.float()).abs().max().item() <= 2e-2 * unfused.float().abs().max().item()
     h = x.to(torch.bfloat16).float() @ w.to(torch.bfloat16).float().t() + b
@@ -332,7 +332,7 @@ def test_linear_fused_geglu(gpu, rows, cin, inner):
     err = (fused.float().cpu() - ref).abs().max().item()
     assert err <= 3e-2 * ref.abs().max().item(), err
     with pytest.raises(ValueError):
-        ops.linear(xb, st.conv_geglu("ff"), geglu=True, act=ops.GELU)
+        ops.linear(xb, st.conv_geglu("ff"), geglu=True, act=ops.GELU, images=1)
 
 
 

@@ -57,3 +57,40 @@ def test_concurrent_sessions_match_single_session(gpu):
     with torch.cuda.stream(streams[1]):
         with pytest.raises(RuntimeError, match="different stream"):
             sessions[0].codec_images(imgs, ctx, noise, steps=2)
+
+
+def test_eager_sessions_in_threads_keep_entropy_split(gpu):
+    """Eager (no plan) sessions on concurrent threads: the bf16 entropy nets' split-K switch is
+    per thread (ops.splitk_allowed), so one session leaving its region never turns split-K off under
+    another's — every thread's bitstreams and pixels equal the single-thread ones."""
+    from rdeic_amd.rdeic import RDEIC
+    m = RDEIC(compute_dtype=torch.bfloat16).init_synthetic()
+    m.use_plans = False
+    imgs, noise, ctx = _inputs()
+    ref_out, ref_bodies = m.codec_images(imgs, ctx, noise, steps=2)
+    sessions = [m.session() for _ in range(3)]
+    for s in sessions:
+        s.use_plans = False
+    streams = [torch.cuda.Stream() for _ in sessions]
+    results, errors = {}, []
+
+    def run(j):
+        try:
+            with torch.cuda.stream(streams[j]):
+                for r in range(2):
+                    out, bodies = sessions[j].codec_images(imgs, ctx, noise, steps=2)
+                    torch.cuda.current_stream().synchronize()
+                    results[(j, r)] = (out.cpu(), bodies)
+        except BaseException as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=(j,)) for j in range(len(sessions))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    assert len(results) == 6
+    for (j, r), (out, bodies) in results.items():
+        assert bodies == ref_bodies, (j, r)
+        assert torch.equal(out, ref_out.cpu()), (j, r)
