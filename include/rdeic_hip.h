@@ -317,6 +317,16 @@ int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row);
 #define RDEIC_PROF_GEMM 5        /* rdeic_gemm_strided (training backward / attention): 2*M*N*K*batch FLOPs */
 #define RDEIC_PROF_ATTN_D512 6   /* rdeic_attention, head dim 512 (VAE AttnBlock flash kernel): 4*B*Lq*Lk*512 FLOPs */
 int rdeic_prof_start(int32_t capacity, int32_t every);
+/* Launch counters (always on, one relaxed atomic add per launch): which kernel a dispatcher chose,
+ * so tests can assert that a fused path actually ran (e.g. the halo conv, not its fallback). */
+#define RDEIC_COUNT_HALO_CONV 0    /* conv3x3_halo_kernel (GroupNorm-input 3x3 convs, VAE geometry) */
+#define RDEIC_COUNT_GN_APPLY 1     /* rdeic_groupnorm_apply kernels */
+#define RDEIC_COUNT_LAYERNORM 2    /* rdeic_layernorm kernels */
+#define RDEIC_COUNT_HALO_SMALL 3   /* the small-image halo conv (UNet / control ResBlocks) */
+#define RDEIC_COUNT_LN_FUSED 4     /* linears with the LayerNorm applied to their A operand */
+#define RDEIC_COUNT_KINDS 8
+int64_t rdeic_launch_count(int32_t kind);
+int rdeic_launch_count_reset(void);
 int rdeic_prof_stop(void);
 int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms);
 

@@ -73,6 +73,8 @@ PROTOTYPES = {
     "rdeic_conv2d_tile": (C.c_int, [C.POINTER(ConvDesc), _i32, _p]),
     "rdeic_prof_start": (C.c_int, [_i32, _i32]),
     "rdeic_prof_stop": (C.c_int, []),
+    "rdeic_launch_count": (C.c_int64, [_i32]),
+    "rdeic_launch_count_reset": (C.c_int, []),
     "rdeic_prof_read": (C.c_int, [_i32, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rdeic_groupnorm_ws_floats": (_sz, [_i32, _i32, _i32]),
     "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p,

@@ -1468,6 +1468,7 @@ int launch_halo(const rdeic_conv_desc* d, ConvArgs a, hipStream_t s, bool* fused
     const unsigned bw = (unsigned)((long)d->cout * d->wld * 2);
     const int tx = d->w / TC, ty = d->h / TR;
     const long tiles = (long)e.n * ty * tx * (d->cout / BN);
+    rdeic_count_launch(RDEIC_COUNT_HALO_CONV);
     if (e.gn_ab)
       hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
     else

@@ -571,6 +571,7 @@ extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32
   if (!x || !ab || !y || n <= 0 || hw <= 0 || c <= 0 || ab_c < c) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps(s, RDEIC_PROF_GN_APPLY, 2.0 * n * hw * c * (dtype == 1 ? 2 : 4));
+  rdeic_count_launch(RDEIC_COUNT_GN_APPLY);
   long total = (long)n * hw * c;
   if (dtype == 1 && c % 8 == 0 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
       ((uintptr_t)y) % 16 == 0 && ((uintptr_t)ab) % 16 == 0 && (ab_c % 2) == 0 &&
@@ -601,6 +602,7 @@ extern "C" int rdeic_layernorm(const void* x, int32_t rows, int32_t c, int32_t l
                                const float* beta, float eps, void* y, int32_t yld, int32_t dtype, void* stream) {
   if (!x || !y || !gamma || !beta || rows <= 0 || c <= 0) return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  rdeic_count_launch(RDEIC_COUNT_LAYERNORM);
   if (dtype == 1 && c % 8 == 0 && c <= 2048 && ld % 8 == 0 && yld % 8 == 0 && ((uintptr_t)x) % 16 == 0 &&
       ((uintptr_t)y) % 16 == 0 && ((uintptr_t)gamma) % 16 == 0 && ((uintptr_t)beta) % 16 == 0)
     hipLaunchKernelGGL(layernorm_vec_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, (const bf16*)x, rows, c, ld, gamma,

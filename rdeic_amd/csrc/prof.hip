@@ -5,12 +5,29 @@
 // read-out is a Horvitz-Thompson estimate: launches = sum w, work = sum w*work, ms = sum w*t.
 // The large launches carry most of the time, so the estimate's variance comes only from the
 // small-launch tail.
+#include <atomic>
 #include <mutex>
 #include <vector>
 
 #include "common.h"
 #include "prof.h"
 #include "../../include/rdeic_hip.h"
+
+std::atomic<long long> g_launch_counts[RDEIC_COUNT_KINDS];
+
+void rdeic_count_launch(int kind) {
+  if (kind >= 0 && kind < RDEIC_COUNT_KINDS) g_launch_counts[kind].fetch_add(1, std::memory_order_relaxed);
+}
+
+extern "C" int64_t rdeic_launch_count(int32_t kind) {
+  if (kind < 0 || kind >= RDEIC_COUNT_KINDS) return RDEIC_EINVAL;
+  return g_launch_counts[kind].load(std::memory_order_relaxed);
+}
+
+extern "C" int rdeic_launch_count_reset(void) {
+  for (auto& c : g_launch_counts) c.store(0, std::memory_order_relaxed);
+  return RDEIC_OK;
+}
 
 namespace {
 struct Slot { hipEvent_t a = nullptr, b = nullptr; int kind = -1; double work = 0.0; double weight = 1.0; };

@@ -494,6 +494,19 @@ HALO_CONV = 1
 HALO_MAX_C = 512
 
 
+# launch counters of the library (rdeic_launch_count, RDEIC_COUNT_* in include/rdeic_hip.h)
+COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED = 0, 1, 2, 3, 4
+
+
+def launch_count(kind: int) -> int:
+    """Launches of one kernel family since the last launch_count_reset (host-side counter)."""
+    return int(_lib.load().rdeic_launch_count(int(kind)))
+
+
+def launch_count_reset() -> None:
+    call("rdeic_launch_count_reset")
+
+
 def set_halo_conv(mode: int) -> int:
     global HALO_CONV
     prev = HALO_CONV

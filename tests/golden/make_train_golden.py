@@ -2,8 +2,8 @@
 own modules and torch autograd on CPU, fp32, at 128x128 (16x16 latent), batch 1.
 
 Run in the development container only (the reference does not exist on the GPU box):
-    python -m tests.golden.make_train_golden
-Output (committed): tests/golden/train_128.npz.
+    python -m tests.golden.make_train_golden [SIZE]
+Output (committed): tests/golden/train_128.npz, and train_512.npz at config 5's own size (r04).
 
 The step restates LatentDiffusion.get_input (ddpm.py:777-833: encode_hc under no_grad, the
 posterior sample x 0.18215, h = c x 0.18215) + RDEIC.get_input (model/rdeic.py:678-686: the
@@ -42,7 +42,7 @@ from tests.golden import refload  # noqa: E402
 from tests.golden.make_golden import fill_module, schedule  # noqa: E402
 from tests.golden.train_proj import projections  # noqa: E402
 
-SIZE = 128
+SIZE = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 SEED = 5
 L_GUIDE, L_BPP, LR = 3.0, 1.0, 2e-5
 FULL_GRADS = ("control_model.control_model.input_blocks.0.0.weight", "control_model.enc_zero_convs_out.0.0.weight",
@@ -123,9 +123,12 @@ def main():
     for k, v in dict(loss=loss, l_simple=loss_simple.mean(), l_bpp=bpp, q_bpp=q_bpp, l_emb=emb_loss,
                      l_guide=loss_guide).items():
         out["loss_" + k] = np.float64(v.item())
-    out.update(x_start=x_start.numpy(), h=h.numpy(), c_latent=c_latent.detach().numpy(),
-               guide_hint=guide_hint.detach().numpy(), x_noisy=x_noisy.detach().numpy(), eps=eps.detach().numpy(),
-               y_lik=lik[0].detach().numpy(), lamba=np.float32(lamba.item()))
+    # above 128^2 the spatial intermediates are stored on a stride-SUB pixel grid (the whole 512^2 set
+    # would be 16 MB); the GPU test subsamples its own tensors the same way
+    sub = 1 if SIZE <= 128 else 4
+    sp = lambda t: np.ascontiguousarray(t.detach().numpy()[:, :, ::sub, ::sub])  # noqa: E731
+    out.update(x_start=sp(x_start), h=sp(h), c_latent=sp(c_latent), guide_hint=sp(guide_hint), x_noisy=sp(x_noisy),
+               eps=sp(eps), y_lik=sp(lik[0]), lamba=np.float32(lamba.item()), subsample=np.int64(sub))
     q = comp.quantize
     out["vq_embed_prob"] = q.embed_prob.numpy().copy()
     out["vq_E_after_fwd_rowsum"] = E_after_fwd.double().sum(1).numpy()
@@ -155,7 +158,7 @@ def main():
             out["after_adamw:" + full] = p.detach().numpy().copy()
     out["after_adamw_E_rowsum"] = comp.quantize.embedding.weight.detach().double().sum(1).numpy()
     # the reference's own AdamW and the restated one agree (the restatement is what the GPU test mirrors)
-    path = os.path.join(HERE, "train_128.npz")
+    path = os.path.join(HERE, f"train_{SIZE}.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, f"{os.path.getsize(path) / 1e6:.2f} MB; {len(names)} trainable tensors, "
           f"{sum(p.numel() for _, p in params) / 1e6:.2f}M params")

@@ -98,3 +98,32 @@ def test_config3_bf16_batch8_self_consistent_and_batch_invariant(gpu):
     out1, _ = m16.codec_images(imgs[1:2], ctx, noise[1:2], steps=5)
     assert torch.equal(out1[0], out[1])  # one image alone decodes to its in-batch pixels
     print("config-3 bpp:", [round(8.0 * len(b) / SIZE ** 2, 4) for b in bodies])
+
+
+def test_config3_fp32_noise_estimator_vs_reference(gpu):
+    """Config 3's relay denoiser in fp32 at latent 128^2 (the UNet's first-level self-attention at
+    L = 16384, d = 64): one NoiseEstimator call (control + SD-2.1 UNet, model/rdeic.py:174-212) at t = 151
+    against the REFERENCE's own modules on the same inputs (tests/golden/eps_1024.npz, made by
+    tests/golden/make_eps1024_golden.py): eps within 1e-3 relative to its largest magnitude."""
+    import os
+    from rdeic_amd import ops
+    from rdeic_amd.rdeic import RDEIC
+    from rdeic_amd.synthetic import synth_context
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "eps_1024.npz"))
+    m32 = RDEIC(compute_dtype=torch.float32).init_synthetic()
+    lat = SIZE // 8
+
+    def field(ch, seed, scale):
+        return ops.fill_uniform(torch.empty(ch * lat * lat, dtype=torch.float32, device="cuda"), int(seed),
+                                float(scale), 0.0).view(1, lat, lat, ch)
+
+    x = field(4, g["x_seed"], g["x_scale"])
+    hint = field(256, g["hint_seed"], g["hint_scale"])
+    t = torch.full((1,), int(g["t"]), dtype=torch.long, device="cuda")
+    with torch.no_grad():
+        e = m32.eps_nhwc(x, t, hint, synth_context().cuda())[0].float().cpu().numpy()
+    ref = g["eps"]
+    rel = np.abs(e - ref).max() / np.abs(ref).max()
+    print(f"1024^2 eps vs reference: max abs err {np.abs(e - ref).max():.2e}, rel {rel:.2e}, "
+          f"mean abs err {np.abs(e - ref).mean():.2e}")
+    assert rel < 1e-3

@@ -1,6 +1,6 @@
 """Adapter fine-tune step (config 5, §8f rank 1) against the reference's own autograd.
 
-tests/golden/train_128.npz holds one step of the REFERENCE modules (UNetModel frozen, NoiseEstimator,
+tests/golden/train_128.npz and train_512.npz (config 5's own size) hold one step of the REFERENCE modules (UNetModel frozen, NoiseEstimator,
 Compression in training mode, VAE encoder; torch autograd, fp32, CPU; tests/golden/make_train_golden.py)
 at 128x128 with the same synthetic weights and seeded draws. The HIP path runs the same step in fp32
 parity mode through the C ABI (forward and backward kernels) and must reproduce:
@@ -16,21 +16,23 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-GOLD = "tests/golden/train_128.npz"
+GOLD = "tests/golden/train_{}.npz"
 TOL = 2e-3
 
 
-@pytest.fixture(scope="module")
-def step():
+# 128^2 (fast) and config 5's own 512^2 (train.py:10-28, configs/finetune_ood.yaml: out_size 512)
+@pytest.fixture(scope="module", params=[128, 512])
+def step(request):
     from rdeic_amd.finetune import FineTuner, nchw_draws_to_nhwc
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import synth_context, synth_image, train_draws
-    g = np.load(GOLD)
+    size = request.param
+    g = np.load(GOLD.format(size))
     m = RDEIC(compute_dtype=torch.float32).init_synthetic()
     ft = FineTuner(m)
-    dr = train_draws(1, 16, 16, m.cfg["compression"]["slice_ch"], 5, m.used_timesteps)
+    dr = train_draws(1, size // 8, size // 8, m.cfg["compression"]["slice_ch"], 5, m.used_timesteps)
     assert np.array_equal(dr["t"].numpy(), g["t"]) and np.array_equal(dr["noise"].numpy(), g["noise"])
-    img = torch.from_numpy(synth_image(128, 128, 231)).cuda()[None]
+    img = torch.from_numpy(synth_image(size, size, 231)).cuda()[None]
     ctx = synth_context().cuda()
     d = nchw_draws_to_nhwc(dr, "cuda")
     ft.zero_grad()
@@ -45,7 +47,8 @@ def step():
     torch.cuda.synchronize()
     params = {n: ft.flat[o:o + k].cpu() for n, (o, k) in ft.offsets.items()}
     fw = dict(x_start=x_start, h=h, **ft._last)
-    fw = {k: v.detach().permute(0, 3, 1, 2).float().cpu().numpy() for k, v in fw.items()}
+    sub = int(g["subsample"]) if "subsample" in g.files else 1  # train_512.npz: stride-4 pixel grid
+    fw = {k: v.detach().permute(0, 3, 1, 2).float().cpu().numpy()[:, :, ::sub, ::sub] for k, v in fw.items()}
     return dict(g=g, ft=ft, ld={k: float(v.detach()) for k, v in ld.items()}, grads=grads, params=params, fw=fw,
                 E_after_fwd=E_after_fwd, ep=ep)
 
@@ -120,7 +123,7 @@ def test_adamw_update(step):
            g["after_adamw_E_rowsum"], 1e-3, "codebook after AdamW")
 
 
-def _run_step(dtype, seed_img=231, seed_draw=5, ddp=False):
+def _run_step(dtype, seed_img=231, seed_draw=5, ddp=False, size=128):
     from rdeic_amd.finetune import FineTuner, nchw_draws_to_nhwc
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import synth_context, synth_image, train_draws
@@ -128,20 +131,21 @@ def _run_step(dtype, seed_img=231, seed_draw=5, ddp=False):
     ft = FineTuner(m)
     if ddp:
         ft.enable_ddp(bucket_bytes=8 << 20)
-    dr = train_draws(1, 16, 16, m.cfg["compression"]["slice_ch"], seed_draw, m.used_timesteps)
-    img = torch.from_numpy(synth_image(128, 128, seed_img)).cuda()[None]
+    dr = train_draws(1, size // 8, size // 8, m.cfg["compression"]["slice_ch"], seed_draw, m.used_timesteps)
+    img = torch.from_numpy(synth_image(size, size, seed_img)).cuda()[None]
     d = ft.training_step(img, synth_context().cuda(), nchw_draws_to_nhwc(dr, "cuda"))
     torch.cuda.synchronize()
     return ft, {k: float(v.detach()) for k, v in d.items()}
 
 
-def test_bf16_step_tracks_the_reference(gpu):
+@pytest.mark.parametrize("size", [128, 512])
+def test_bf16_step_tracks_the_reference(gpu, size):
     """The bf16 training path (the throughput mode) against the fp32 reference step: loss terms within
     bf16 tolerance and the gradient directions of the large majority of tensors (bf16 activations
-    through ~100 layers; the VQ / rounding decisions of the entropy model may flip)."""
-    from tests.golden.train_proj import projections
-    g = np.load(GOLD)
-    ft, ld = _run_step(torch.bfloat16)
+    through ~100 layers; the VQ / rounding decisions of the entropy model may flip). 512^2 is config 5's
+    own size (bench_train.py's step)."""
+    g = np.load(GOLD.format(size))
+    ft, ld = _run_step(torch.bfloat16, size=size)
     assert all(np.isfinite(v) for v in ld.values())
     for ours, ref, tol in (("T/l_simple", "loss_l_simple", 0.1), ("T/l_guide", "loss_l_guide", 0.05),
                            ("T/l_bpp", "loss_l_bpp", 0.05), ("T/l_emb", "loss_l_emb", 0.1)):
@@ -245,19 +249,21 @@ def test_two_rank_ddp_step_equals_averaged_gradients(gpu):
     assert diff <= 1e-7, diff
 
 
-def test_captured_step_replays_the_eager_steps(gpu):
+@pytest.mark.parametrize("dtype,size", [(torch.float32, 128), (torch.bfloat16, 512)])
+def test_captured_step_replays_the_eager_steps(gpu, dtype, size):
     """CapturedStep (the whole step as one hipGraph) reproduces two eager steps bit for bit:
-    parameters, AdamW moments, VQ usage EMA and the loss dict."""
+    parameters, AdamW moments, VQ usage EMA and the loss dict. bf16 at 512^2 is bench_train.py's
+    step (config 5): its losses must also be finite."""
     from rdeic_amd.finetune import CapturedStep, FineTuner, nchw_draws_to_nhwc
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import synth_context, synth_image, train_draws
     ctx = synth_context().cuda()
-    imgs = [torch.from_numpy(synth_image(128, 128, 300 + i)).cuda()[None] for i in range(2)]
+    imgs = [torch.from_numpy(synth_image(size, size, 300 + i)).cuda()[None] for i in range(2)]
     runs = []
     for captured in (False, True):
-        m = RDEIC(compute_dtype=torch.float32).init_synthetic()
+        m = RDEIC(compute_dtype=dtype).init_synthetic()
         ft = FineTuner(m)
-        draws = [nchw_draws_to_nhwc(train_draws(1, 16, 16, m.cfg["compression"]["slice_ch"], 40 + i,
+        draws = [nchw_draws_to_nhwc(train_draws(1, size // 8, size // 8, m.cfg["compression"]["slice_ch"], 40 + i,
                                                 m.used_timesteps), "cuda") for i in range(2)]
         cs = CapturedStep(ft, imgs[0], ctx, draws[0]) if captured else None
         losses = []
@@ -269,3 +275,4 @@ def test_captured_step_replays_the_eager_steps(gpu):
     (p0, m0, v0, e0, l0), (p1, m1, v1, e1, l1) = runs
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1) and torch.equal(e0, e1)
     assert l0 == l1
+    assert all(np.isfinite(v) for d in l0 for v in d.values())

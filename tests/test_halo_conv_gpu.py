@@ -36,7 +36,11 @@ def _run(x, p, ab, silu=True, res=None, stats=False, halo=True):
     prev = ops.set_halo_conv(1 if halo else 0)
     prev_c, ops.HALO_MAX_C = ops.HALO_MAX_C, 512  # every width the kernel supports, not only the ones it wins
     try:
-        return ops.conv2d(x, p, gn=ab, gn_silu=silu, res=res, stats=stats)
+        n0 = ops.launch_count(ops.COUNT_HALO_CONV)
+        y = ops.conv2d(x, p, gn=ab, gn_silu=silu, res=res, stats=stats)
+        # the library's own dispatch took the halo kernel (not a silent fallback to the apply + im2col path)
+        assert (ops.launch_count(ops.COUNT_HALO_CONV) > n0) == halo
+        return y
     finally:
         ops.set_halo_conv(prev)
         ops.HALO_MAX_C = prev_c
