@@ -1257,6 +1257,18 @@ struct Rows {  // tile row r (wave row r / 64, column r % 64) -> output pixel
 };
 }  // namespace halo
 
+#ifdef RDEIC_HALO_STAMPS
+// diagnostic build only (tools/halo_stamps.hip): per-block shader-clock stamps, 8 u64 per block,
+// written by thread 0 with ordinary vector stores into a buffer nothing else reads
+__device__ unsigned long long* g_halo_stamps;
+#define HALO_STAMP(k)                                                                      \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_halo_stamps[(long)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define HALO_STAMP(k) do {} while (0)
+#endif
+
 template <bool GN>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3x3_halo_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
                                                                unsigned bytesw) {
@@ -1265,6 +1277,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   char* const hbuf = lds;
   char* const bbuf = lds + 2 * HBYTES;
   float* const abl = reinterpret_cast<float*>(lds + 2 * HBYTES + NB * BBYTES);
+  HALO_STAMP(0);
+#ifdef RDEIC_HALO_STAMPS
+  if (threadIdx.x == 0) {
+    g_halo_stamps[(long)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    g_halo_stamps[(long)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
+#endif
   const int tn = a.cout / BN;
   // XCD-aware bijective remap (as conv_dma_body): an XCD owns a contiguous run of tile ids, the N
   // tiles of one image block adjacent (they share its halo through L2)
@@ -1382,6 +1401,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   wait_vm<2>();  // this wave's halo pieces
   if constexpr (GN) transform(0);
 
+  HALO_STAMP(1);
   const int lr = lane & 15, lq = lane >> 4;
   const int bsw = (lq ^ sw(lr)) * 16;  // weight rows n = 64 wn + 16 j + lr share sw(lr)
   // A fragment i of a tap reads halo slots s0 + 16 i + lr: adding 16 leaves bits 0..3 (and so the
@@ -1430,8 +1450,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       }
     }
   }
+  HALO_STAMP(2);
   epilogue_vec<TR * TC, BN, 4, 2, NT, 2>(acc, a, 0, n0, wm, wn, lane, tid, lds,
                                          Rows{(img * H + oy0) * W + ox0, W});
+  HALO_STAMP(3);
 }
 
 int g_halo = 1;  // 3x3 halo conv: 0 off, 1 for GroupNorm-input convs (default), 2 for every eligible conv

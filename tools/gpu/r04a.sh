@@ -3,6 +3,11 @@
 set -o pipefail
 O=gpurun_out/r04a
 mkdir -p $O
+for cfg in "16 512 512 128 128 1 1" "16 512 512 128 128 0 0" "16 512 512 128 128 1 0" "16 512 512 128 128 0 1" \
+           "16 256 256 256 256 1 1" "16 128 128 512 512 1 1"; do
+  timeout -k 5 60 tools/halo_stamps $cfg >> $O/halo_stamps.jsonl 2>> $O/halo_stamps.err || { echo "halo_stamps failed"; exit 3; }
+done
+cat $O/halo_stamps.jsonl
 timeout -k 10 1200 python -u -m pytest -v --timeout 400 --timeout-method thread \
   tests/test_halo_conv_gpu.py tests/test_config3_gpu.py::test_config3_fp32_noise_estimator_vs_reference \
   tests/test_bf16_vs_fp32_gpu.py tests/test_finetune_gpu.py tests/test_sessions_gpu.py > $O/pytest.log 2>&1

@@ -43,7 +43,7 @@ def main():
         for t in TILES:
             ops.FORCE_TILE = t if t >= 0 else None
             try:
-                fn = lambda: ops.linear(x, p, res=r, out=out, geglu=geglu)  # noqa: E731
+                fn = lambda: ops.linear(x, p, res=r, out=out, geglu=geglu, images=16)  # noqa: E731
                 fn()
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
