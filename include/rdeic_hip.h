@@ -78,6 +78,13 @@ typedef struct rdeic_conv_desc {
   int32_t gn_hw;        /* pixels per image of the GroupNorm those statistics feed (divides n*ho*wo;
                            differs from ho*wo when a linear's rows are an image's tokens) */
   int32_t reserved;
+  /* LayerNorm folded into a linear (bf16, out_mode 0 / 2, batch 1; attention.py:273-285 norm1/2/3 ->
+   * to_q/k/v / to_q / ff.net.0.proj): the GEMM runs on the RAW rows x with weights diag(gamma) W and
+   * the epilogue computes, before the bias, v = rstd_m * (acc - mean_m * ln_colsum[n]);
+   * bias = bias + W beta. ln_rows: [M][2] fp32 (mean, rstd) from rdeic_layernorm_rowstats,
+   * ln_colsum: [cout] fp32 column sums of the packed bf16 weight. NULL: off. */
+  const float* ln_rows;
+  const float* ln_colsum;
 } rdeic_conv_desc;
 
 int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
@@ -323,9 +330,15 @@ int rdeic_prof_start(int32_t capacity, int32_t every);
 #define RDEIC_COUNT_GN_APPLY 1     /* rdeic_groupnorm_apply kernels */
 #define RDEIC_COUNT_LAYERNORM 2    /* rdeic_layernorm kernels */
 #define RDEIC_COUNT_HALO_SMALL 3   /* the small-image halo conv (UNet / control ResBlocks) */
-#define RDEIC_COUNT_LN_FUSED 4     /* linears with the LayerNorm applied to their A operand */
+#define RDEIC_COUNT_LN_FUSED 4     /* rdeic_layernorm_rowstats (LayerNorm folded into the next linear) */
 #define RDEIC_COUNT_KINDS 8
 int64_t rdeic_launch_count(int32_t kind);
+/* Per-row LayerNorm statistics (attention.py:273-285, torch.nn.LayerNorm: biased variance, eps) of
+ * bf16 rows x[rows][c] (pixel stride ld): ms[2 r] = mean, ms[2 r + 1] = 1 / sqrt(var + eps), two-pass
+ * in registers. The folded linear (rdeic_conv_desc.ln_rows) consumes them; replaces rdeic_layernorm's
+ * normalised tensor (never written). c % 8 == 0, c <= 2048. */
+int rdeic_layernorm_rowstats(const void* x, int32_t rows, int32_t c, int32_t ld, float eps, float* ms,
+                             void* stream);
 int rdeic_launch_count_reset(void);
 int rdeic_prof_stop(void);
 int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms);

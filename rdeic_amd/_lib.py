@@ -47,6 +47,7 @@ class ConvDesc(C.Structure):
         ("dtype", C.c_int32), ("out_f32", C.c_int32),
         ("batch", C.c_int32), ("in_bs", C.c_int64), ("w_bs", C.c_int64), ("out_bs", C.c_int64),
         ("gn_part", C.c_void_p), ("gn_hw", C.c_int32), ("reserved", C.c_int32),
+        ("ln_rows", C.c_void_p), ("ln_colsum", C.c_void_p),
     ]
 
 
@@ -75,6 +76,7 @@ PROTOTYPES = {
     "rdeic_prof_stop": (C.c_int, []),
     "rdeic_launch_count": (C.c_int64, [_i32]),
     "rdeic_launch_count_reset": (C.c_int, []),
+    "rdeic_layernorm_rowstats": (C.c_int, [C.c_void_p, _i32, _i32, _i32, C.c_float, C.c_void_p, C.c_void_p]),
     "rdeic_prof_read": (C.c_int, [_i32, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "rdeic_groupnorm_ws_floats": (_sz, [_i32, _i32, _i32]),
     "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p,

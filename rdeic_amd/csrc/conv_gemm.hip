@@ -45,7 +45,16 @@ struct ConvArgs {
   float* gn_part;            // fused GroupNorm statistics of the output (see epilogue_vec), or NULL
   int gn_row0;               // absolute output row of this launch's row 0 (image-group launches)
   int gn_hw;                 // pixels per image of the GroupNorm those statistics feed
+  const float* ln_rows;      // folded LayerNorm: [M][2] (mean, rstd) of the raw input rows, or NULL
+  const float* ln_cs;        // ... and the column sums of the packed (gamma-scaled) bf16 weight
 };
+
+// Folded LayerNorm (rdeic_conv_desc.ln_rows): LN(x) W = rstd (x W' - mean colsum(W')) with W' = diag(gamma) W
+// and beta W in the bias; applied to the raw accumulator before everything else of the epilogue.
+__device__ __forceinline__ float ln_fold(const ConvArgs& a, int m, int n, float v) {
+  const float2 ms = reinterpret_cast<const float2*>(a.ln_rows)[m];
+  return ms.y * (v - ms.x * a.ln_cs[n]);
+}
 
 int g_conv_path = 2;  // 0: 128-tiles with the fused GroupNorm prologue only, 2 (default): big-tile auto choice
 int g_epi_vec = 1;    // LDS-staged vector epilogue (rdeic_set_conv_option(0, v))
@@ -182,6 +191,14 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
       const float4 x0 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8);
       const float4 x1 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8 + 4);
       v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      if (a.ln_rows) {
+        const float2 ms = reinterpret_cast<const float2*>(a.ln_rows)[m];
+        const float4 c0 = *reinterpret_cast<const float4*>(a.ln_cs + nn);
+        const float4 c1 = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4);
+        const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ms.y * (v[e] - ms.x * cs[e]);
+      }
       if (a.bias) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += a.bias[nn + e];
@@ -569,6 +586,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
         const int nn = n0 + wn * WTN + j * 16 + lrow;
         if (nn >= a.cout) continue;
         float v = acc[i][j][r];
+        if (a.ln_rows) v = ln_fold(a, m, nn, v);
         if (a.bias) v += a.bias[nn];
         if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
         v = apply_act(v, a.act, a.act_param);
@@ -788,6 +806,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, const fl
   const int hw_o = a.ho * a.wo;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
+    if (a.ln_rows) v[e] = ln_fold(a, m, nn + e, v[e]);
     if (a.bias) v[e] += a.bias[nn + e];
     if (a.emb) v[e] += a.emb[(long)(m / hw_o) * a.emb_ld + nn + e];
     v[e] = apply_act(v[e], a.act, a.act_param);
@@ -867,6 +886,7 @@ __device__ __forceinline__ void epilogue_scalar(const f32x4 (&acc)[TM][TN], cons
         const int nn = n0 + wn * WTN + j * 16 + lrow;
         if (nn >= a.cout) continue;
         float v = acc[i][j][r];
+        if (a.ln_rows) v = ln_fold(a, m, nn, v);
         if (a.bias) v += a.bias[nn];
         if (a.emb) v += a.emb[(long)img * a.emb_ld + nn];
         v = apply_act(v, a.act, a.act_param);
@@ -1179,7 +1199,7 @@ int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipSt
   if (dma_ok(d, a, b0, b1, bw)) {
     if (splits > 1) {
       a.splits = splits; a.kper = (a.nk + splits - 1) / splits;
-      a.bias = nullptr; a.emb = nullptr; a.act = 0; a.res = nullptr;
+      a.bias = nullptr; a.emb = nullptr; a.act = 0; a.res = nullptr; a.ln_rows = nullptr;
       a.out = (char*)ws; a.out_ld = a.cout; a.out_f32 = 1; a.out_mode = 0;
       a.gn_part = nullptr;
     }
@@ -1202,6 +1222,7 @@ int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipSt
     e.out = (char*)d->out + i0 * opix * d->out_ld * osz;
     e.res = d->res ? (const char*)d->res + i0 * opix * d->res_ld * osz : nullptr;
     e.emb = d->emb ? d->emb + (long)i0 * d->emb_ld : nullptr;
+    e.ln_rows = d->ln_rows ? d->ln_rows + 2l * i0 * d->ho * d->wo : nullptr;
     ConvArgs ea;
     if (make_args(&e, ea, vec) != RDEIC_OK || !vec || !dma_ok(&e, ea, b0, b1, bw)) return -1;
     ea.gn_row0 = i0 * d->ho * d->wo;
@@ -1526,6 +1547,10 @@ int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec) {
   a.epi_vec = g_epi_vec;
   a.splits = 1; a.kper = 0;
   a.gn_part = d->gn_part; a.gn_row0 = 0; a.gn_hw = d->gn_hw;
+  a.ln_rows = d->ln_rows; a.ln_cs = d->ln_colsum;
+  if ((d->ln_rows != nullptr) != (d->ln_colsum != nullptr)) return RDEIC_EINVAL;
+  if (d->ln_rows && (d->dtype != 1 || d->batch > 1 || d->out_mode == 1 || d->gn_ab || ((uintptr_t)d->ln_colsum) % 16))
+    return RDEIC_EINVAL;
   a.M = d->n * d->ho * d->wo;
   a.batch = d->batch > 1 ? d->batch : 1;
   a.in_bs = d->in_bs; a.w_bs = d->w_bs; a.out_bs = d->out_bs;
@@ -1660,7 +1685,7 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
   hipStream_t s = (hipStream_t)stream;
   if (d->dtype == 0) {  // fp32: 64x64 register-staged partial tiles, fp32 output from the reduction
     ConvArgs p = a;
-    p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr;
+    p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr; p.ln_rows = nullptr;
     p.out = (char*)ws; p.out_ld = a.cout; p.out_f32 = 0;
     p.splits = splits;
     p.kper = (a.nk + splits - 1) / splits;
@@ -1682,7 +1707,7 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
     return launch_status();
   }
   ConvArgs p = a;  // partial pass: raw sums into the workspace
-  p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr;
+  p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr; p.ln_rows = nullptr;
   p.out = (char*)ws; p.out_ld = a.cout; p.out_f32 = 1;
   p.splits = splits;
   p.kper = (a.nk + splits - 1) / splits;

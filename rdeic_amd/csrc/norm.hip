@@ -598,6 +598,59 @@ extern "C" int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32
   return launch_status();
 }
 
+// Row statistics of a LayerNorm whose affine is folded into the consuming linear
+// (rdeic_conv_desc.ln_rows): 16 lanes per row, 4 rows per wave, each lane up to 16 chunks of 8 bf16 in
+// registers (one HBM read), mean then the centred sum of squares (two passes over the registers, as
+// rdeic_layernorm computes them), xor-shuffle sums inside the 16-lane group.
+__global__ __launch_bounds__(256) void ln_rowstats_kernel(const bf16* __restrict__ x, int rows, int c, int ld, float eps,
+                                                          float2* __restrict__ ms) {
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int l = threadIdx.x & 15;
+  const int cp = c >> 3;
+  const bool live = row < rows;
+  const bf16* xr = x + (long)(live ? row : 0) * ld;
+  bf16x8 v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int k = l + u * 16;
+    if (live && k < cp) {
+      v[u] = *reinterpret_cast<const bf16x8*>(xr + k * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)v[u][e];
+    }
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / c;
+  float v2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int k = l + u * 16;
+    if (live && k < cp) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (float)v[u][e] - mean;
+        v2 += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v2 += __shfl_xor(v2, o, 64);
+  if (live && l == 0) ms[row] = make_float2(mean, rsqrtf(v2 / c + eps));
+}
+
+extern "C" int rdeic_layernorm_rowstats(const void* x, int32_t rows, int32_t c, int32_t ld, float eps, float* ms,
+                                        void* stream) {
+  if (!x || !ms || rows <= 0 || c <= 0 || c % 8 || c > 2048 || ld % 8 || ((uintptr_t)x) % 16 || ((uintptr_t)ms) % 8)
+    return RDEIC_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  rdeic_count_launch(RDEIC_COUNT_LN_FUSED);
+  hipLaunchKernelGGL(ln_rowstats_kernel, dim3((rows + 15) / 16), dim3(256), 0, s, (const bf16*)x, rows, c, ld, eps,
+                     reinterpret_cast<float2*>(ms));
+  return launch_status();
+}
+
 extern "C" int rdeic_layernorm(const void* x, int32_t rows, int32_t c, int32_t ld, const float* gamma,
                                const float* beta, float eps, void* y, int32_t yld, int32_t dtype, void* stream) {
   if (!x || !y || !gamma || !beta || rows <= 0 || c <= 0) return RDEIC_EINVAL;

@@ -68,6 +68,7 @@ class ConvParams:
     kw: int
     stride: int = 1
     pad: int = 0
+    ln_cs: Optional[torch.Tensor] = None  # folded LayerNorm (ParamStore.conv_ln): column sums of the packed weight
 
     @staticmethod
     def pack(w: torch.Tensor, b: Optional[torch.Tensor], stride: int = 1, pad: int = 0,
@@ -91,14 +92,16 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
            act: int = NONE, slope: float = 0.0, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, pixel_shuffle: bool = False,
            geglu: bool = False, stats: bool = False, stats_hw: Optional[int] = None,
-           images: Optional[int] = None) -> torch.Tensor:
+           images: Optional[int] = None, ln_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = act(conv(cat(x, x2)) + bias + emb) + res   (all NHWC).
     images: how many images the launch covers when that is not n (token rows of ops.linear); the
     inference split-K count is chosen per image (SPLITK_NOMINAL_BATCH).
     geglu: p packed by ParamStore.conv_geglu; out = value * gelu(gate), cout/2 channels (bf16).
     stats: the output feeds a GroupNorm — its statistics are produced with it (fused into the conv
     epilogue where the tile allows, rdeic_conv_desc.gn_part) and group_norm_ab(out) then needs no
-    pass over the tensor. stats_hw: pixels per image of that GroupNorm (default ho*wo)."""
+    pass over the tensor. stats_hw: pixels per image of that GroupNorm (default ho*wo).
+    ln_rows: [M, 2] fp32 (mean, rstd) of the raw input rows from layer_norm_rowstats, with p packed by
+    ParamStore.conv_ln: the output is linear(LayerNorm(x)) (the LayerNorm folded into the GEMM)."""
     if gn is not None and _gn_materialize(x, x2, p) and not _halo_eligible(x, x2, p, up2, pad_t, pad_l, out_hw,
                                                                            geglu or pixel_shuffle, out):
         # the big-tile conv path has no GroupNorm prologue (it is VALU-bound there): materialise the
@@ -173,6 +176,13 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     d.dtype = dt_code(x)
     d.out_f32 = int(odt == torch.float32 and x.dtype != torch.float32)
     d.batch = 1
+    if ln_rows is not None:
+        if p.ln_cs is None or ln_rows.dtype != torch.float32 or tuple(ln_rows.shape) != (n * ho * wo, 2) \
+                or not ln_rows.is_contiguous():
+            raise ValueError("ln_rows needs a ParamStore.conv_ln weight and an fp32 [M, 2] contiguous (mean, rstd)")
+        d.ln_rows, d.ln_colsum = ln_rows.data_ptr(), p.ln_cs.data_ptr()
+    elif p.ln_cs is not None:
+        raise ValueError("a LayerNorm-folded weight needs ln_rows")
     part = None
     if stats and GN_STATS_FUSE and x.dtype == torch.bfloat16 and not (geglu or pixel_shuffle):
         ghw = int(stats_hw or ho * wo)
@@ -550,7 +560,7 @@ def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) 
 
 def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, out_f32: bool = False, geglu: bool = False,
-           stats_hw: Optional[int] = None, images: int) -> torch.Tensor:
+           stats_hw: Optional[int] = None, images: int, ln_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Token-wise Linear over a [rows, c] tensor (1x1 conv over a rows x 1 image).
     images: the number of images whose tokens the rows hold (required: the per-image split-K choice
     keeps every output's k grouping independent of the batch).
@@ -568,7 +578,7 @@ def linear(x: torch.Tensor, p: ConvParams, *, act: int = NONE, res: Optional[tor
     if res is not None:
         r4 = res.as_strided((1, rows, 1, p.cout), (rows * res.stride(0), res.stride(0), res.stride(0), 1))
     conv2d(x4, p, act=act, res=r4, out=o4, out_f32=out_f32, geglu=geglu, stats=stats_hw is not None,
-           stats_hw=stats_hw, images=images)
+           stats_hw=stats_hw, images=images, ln_rows=ln_rows)
     info = getattr(o4, "_rdeic_gn_part", None)
     if info is not None:
         out._rdeic_gn_tokens = info  # carried to the NHWC view by tokens_to_nhwc
@@ -638,6 +648,20 @@ def group_norm_apply(x: torch.Tensor, ab: torch.Tensor, silu: bool, out: Optiona
     _launch(("gn_apply", float(2 * n * h * w * c * x.element_size()), None),
             "rdeic_groupnorm_apply", x.data_ptr(), n, h * w, c, pix_ld(x), ab.data_ptr(),
             ab.stride(0) // 2, int(silu), float(out_mul), out.data_ptr(), pix_ld(out), dt_code(x), stream_ptr())
+    return out
+
+
+# bf16 transformer LayerNorms folded into the consuming linear (rdeic_layernorm_rowstats + conv_ln weights):
+# the normalised tensor is never written
+LN_FOLD = True
+
+
+def layer_norm_rowstats(x: torch.Tensor, eps: float = 1e-5, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[rows, c] bf16 -> [rows, 2] fp32 (mean, 1/sqrt(var + eps)) per row (torch.nn.LayerNorm's statistics)."""
+    rows, c = x.shape
+    if out is None:
+        out = torch.empty((rows, 2), dtype=torch.float32, device=x.device)
+    call("rdeic_layernorm_rowstats", x.data_ptr(), rows, c, x.stride(0), float(eps), out.data_ptr(), stream_ptr())
     return out
 
 

@@ -137,6 +137,35 @@ class ParamStore:
             self._packed[key] = p
         return p
 
+    def conv_ln(self, prefixes: Sequence[str], ln_prefix: str, geglu: bool = False, dtype=None) -> ops.ConvParams:
+        """Linear(s) fed by LayerNorm(ln_prefix) with the LayerNorm folded in (ops.linear(ln_rows=...)):
+        LN(x) W^T + b = rstd (x W'^T - mean colsum(W')) + (b + W beta), W' = W diag(gamma). The packed
+        weight is W' (stacked along cout for several prefixes, or GEGLU-interleaved as conv_geglu);
+        ln_cs holds the column sums of the PACKED bf16 W' (so the mean term cancels what the GEMM
+        accumulated), summed in fp64."""
+        dtype = dtype or self.compute_dtype
+        key = (tuple(prefixes), "ln", ln_prefix, geglu, dtype)
+        p = self._packed.get(key)
+        if p is None:
+            gamma, beta = self.t[ln_prefix + ".weight"], self.t[ln_prefix + ".bias"]
+            ws, bs = [], []
+            for pre in prefixes:
+                w = self.t[pre + ".weight"]
+                b = self.t.get(pre + ".bias")
+                ws.append(w)
+                bs.append(b if b is not None else torch.zeros(w.shape[0], device=self.device))
+            w = torch.cat(ws, 0)
+            b = torch.cat(bs, 0).double() + w.double() @ beta.double()
+            w = w * gamma[None, :]
+            if geglu:
+                c = w.shape[0] // 2
+                perm = torch.arange(2 * c, device=w.device).view(2, c // 4, 4).permute(1, 0, 2).reshape(-1)
+                w, b = w[perm], b[perm]
+            p = ops.ConvParams.pack(w, b.float(), dtype=dtype)
+            p.ln_cs = p.weight.double().sum(1).float().contiguous()
+            self._packed[key] = p
+        return p
+
     def conv_cat(self, prefixes: Sequence[str], dtype=None) -> ops.ConvParams:
         """Several layers with the same input stacked along cout (one GEMM: q|k|v, k|v, emb_layers)."""
         dtype = dtype or self.compute_dtype

@@ -222,26 +222,40 @@ class UNet:
         h4 = ops.conv2d(x, s.conv(t.prefix + ".proj_in"), gn=ab, gn_silu=False)
         h = h4.view(rows, C)
         scale = t.dh ** -0.5
+        # LayerNorms folded into the linears they feed (bf16): row statistics only, no normalised tensor
+        fold = x.dtype == torch.bfloat16 and ops.LN_FOLD and C % 64 == 0
         # self-attention
-        n1 = ops.layer_norm(h, s.get(tb + ".norm1.weight"), s.get(tb + ".norm1.bias"))
-        qkv = ops.linear(n1, s.conv_cat([tb + ".attn1.to_q", tb + ".attn1.to_k", tb + ".attn1.to_v"]), images=B)
+        qkv_names = [tb + ".attn1.to_q", tb + ".attn1.to_k", tb + ".attn1.to_v"]
+        if fold:
+            qkv = ops.linear(h, s.conv_ln(qkv_names, tb + ".norm1"), ln_rows=ops.layer_norm_rowstats(h), images=B)
+        else:
+            n1 = ops.layer_norm(h, s.get(tb + ".norm1.weight"), s.get(tb + ".norm1.bias"))
+            qkv = ops.linear(n1, s.conv_cat(qkv_names), images=B)
         o = torch.empty((rows, C), dtype=x.dtype, device=x.device)
         ops.attention(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, batch=B, heads=t.heads, lq=L, lk=L, dh=t.dh,
                       scale=scale)
         h = ops.linear(o, s.conv(tb + ".attn1.to_out.0"), res=h, images=B)
         # cross-attention against the text context
-        n2 = ops.layer_norm(h, s.get(tb + ".norm2.weight"), s.get(tb + ".norm2.bias"))
-        q = ops.linear(n2, s.conv(tb + ".attn2.to_q"), images=B)
+        if fold:
+            q = ops.linear(h, s.conv_ln([tb + ".attn2.to_q"], tb + ".norm2"), ln_rows=ops.layer_norm_rowstats(h),
+                           images=B)
+        else:
+            n2 = ops.layer_norm(h, s.get(tb + ".norm2.weight"), s.get(tb + ".norm2.bias"))
+            q = ops.linear(n2, s.conv(tb + ".attn2.to_q"), images=B)
         kv = ops.linear(ctx_kv_in, s.conv_cat([tb + ".attn2.to_k", tb + ".attn2.to_v"]), images=ctx_batch)
         ops.attention(q, kv[:, :C], kv[:, C:], o, batch=B, heads=t.heads, lq=L, lk=ctx_len, dh=t.dh, scale=scale,
                       kv_bcast=(ctx_batch == 1 and B > 1))
         h = ops.linear(o, s.conv(tb + ".attn2.to_out.0"), res=h, images=B)
         # GEGLU feed-forward
-        n3 = ops.layer_norm(h, s.get(tb + ".norm3.weight"), s.get(tb + ".norm3.bias"))
-        if x.dtype == torch.bfloat16 and ops.GEGLU_FUSED and C % 64 == 0:
-            gg = ops.linear(n3, s.conv_geglu(tb + ".ff.net.0.proj"), geglu=True, images=B)  # one pass, half the writes
+        if fold and ops.GEGLU_FUSED:
+            gg = ops.linear(h, s.conv_ln([tb + ".ff.net.0.proj"], tb + ".norm3", geglu=True),
+                            ln_rows=ops.layer_norm_rowstats(h), geglu=True, images=B)
         else:
-            gg = ops.geglu(ops.linear(n3, s.conv(tb + ".ff.net.0.proj"), images=B))
+            n3 = ops.layer_norm(h, s.get(tb + ".norm3.weight"), s.get(tb + ".norm3.bias"))
+            if x.dtype == torch.bfloat16 and ops.GEGLU_FUSED and C % 64 == 0:
+                gg = ops.linear(n3, s.conv_geglu(tb + ".ff.net.0.proj"), geglu=True, images=B)  # one pass, half the writes
+            else:
+                gg = ops.geglu(ops.linear(n3, s.conv(tb + ".ff.net.0.proj"), images=B))
         h = ops.linear(gg, s.conv(tb + ".ff.net.2"), res=h, images=B)
         # proj_out + residual to the block input
         if not x.is_contiguous():

@@ -360,3 +360,57 @@ def test_attention_dh64_kernels(gpu, mode, heads, lq, lk, bcast):
     ref = _ref_attn(qf, kf.expand(B, -1, -1).contiguous(), vf.expand(B, -1, -1).contiguous(), heads, dh, dh ** -0.5)
     err = (o.float().cpu().view(B, lq, -1) - ref).abs().max().item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("rows,cin,couts,geglu", [(4096, 320, (320, 320, 320), False), (1024, 640, (640,), False),
+                                                  (512, 1280, (2 * 5120,), True), (77 * 3, 320, (320,), False)])
+def test_layernorm_folded_linear(gpu, rows, cin, couts, geglu):
+    """LayerNorm folded into the linear it feeds (ParamStore.conv_ln + rdeic_layernorm_rowstats, the bf16
+    transformer's norm1/2/3 -> to_qkv / to_q / ff.net.0.proj, attention.py:273-285): against the
+    materialised LayerNorm + linear and against torch fp32 LayerNorm + Linear."""
+    import torch.nn.functional as F
+    from rdeic_amd import ops
+    from rdeic_amd.params import ParamStore
+    g = torch.Generator().manual_seed(rows + cin)
+    x = (torch.randn(rows, cin, generator=g) * 1.7 + 0.4).to(torch.bfloat16)
+    gamma = 1 + 0.3 * torch.randn(cin, generator=g)
+    beta = 0.2 * torch.randn(cin, generator=g)
+    st = ParamStore(torch.bfloat16, "cuda")
+    names = []
+    ws, bs = [], []
+    for i, co in enumerate(couts):
+        w = torch.randn(co, cin, generator=g) / math.sqrt(cin)
+        b = torch.randn(co, generator=g) * 0.1
+        st.shapes[f"l{i}.weight"], st.shapes[f"l{i}.bias"] = tuple(w.shape), tuple(b.shape)
+        st.t[f"l{i}.weight"], st.t[f"l{i}.bias"] = w.cuda(), b.cuda()
+        names.append(f"l{i}")
+        ws.append(w)
+        bs.append(b)
+    st.shapes["ln.weight"] = st.shapes["ln.bias"] = (cin,)
+    st.t["ln.weight"], st.t["ln.bias"] = gamma.cuda(), beta.cuda()
+    xd = x.cuda()
+    ops.launch_count_reset()
+    ms = ops.layer_norm_rowstats(xd)
+    fused = ops.linear(xd, st.conv_ln(names, "ln", geglu=geglu), ln_rows=ms, geglu=geglu, images=1)
+    assert ops.launch_count(ops.COUNT_LN_FUSED) == 1 and ops.launch_count(ops.COUNT_LAYERNORM) == 0
+    n = ops.layer_norm(xd, gamma.cuda(), beta.cuda())
+    if geglu:
+        unf = ops.linear(n, st.conv_geglu(names[0]), geglu=True, images=1)
+    else:
+        unf = ops.linear(n, st.conv_cat(names), images=1)
+    torch.cuda.synchronize()
+    # statistics: torch's LayerNorm of the bf16 rows in fp32
+    xf = x.float()
+    mean, var = xf.mean(1), xf.var(1, unbiased=False)
+    torch.testing.assert_close(ms.cpu()[:, 0], mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ms.cpu()[:, 1], torch.rsqrt(var + 1e-5), rtol=1e-5, atol=1e-5)
+    nf = F.layer_norm(xf, (cin,), gamma, beta, 1e-5)
+    h = nf @ torch.cat(ws).t() + torch.cat(bs)
+    ref = h[:, : h.shape[1] // 2] * F.gelu(h[:, h.shape[1] // 2:]) if geglu else h
+    scale = ref.abs().max().item()
+    e_f = (fused.float().cpu() - ref).abs()
+    e_u = (unf.float().cpu() - ref).abs()
+    print(f"folded: max {e_f.max().item():.3e} mean {e_f.mean().item():.3e}; materialised: max {e_u.max().item():.3e} "
+          f"mean {e_u.mean().item():.3e} (ref max {scale:.2f})")
+    assert e_f.max().item() <= 2e-2 * scale
+    assert e_f.mean().item() <= 1.5 * e_u.mean().item() + 1e-4  # no worse than the bf16 materialised path

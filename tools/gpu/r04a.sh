@@ -10,7 +10,7 @@ done
 cat $O/halo_stamps.jsonl
 timeout -k 10 1200 python -u -m pytest -v --timeout 400 --timeout-method thread \
   tests/test_halo_conv_gpu.py tests/test_config3_gpu.py::test_config3_fp32_noise_estimator_vs_reference \
-  tests/test_bf16_vs_fp32_gpu.py tests/test_finetune_gpu.py tests/test_sessions_gpu.py > $O/pytest.log 2>&1
+  tests/test_bf16_vs_fp32_gpu.py tests/test_finetune_gpu.py tests/test_sessions_gpu.py "tests/test_kernels_gpu.py::test_layernorm_folded_linear" > $O/pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
