@@ -1276,7 +1276,129 @@ struct Rows {  // tile row r (wave row r / 64, column r % 64) -> output pixel
   int base, W;
   __device__ __forceinline__ int operator()(int r) const { return base + (r >> 6) * W + (r & 63); }
 };
+
+// Epilogue LDS plan (four passes of 64 tile rows: one 16-row fragment per wave row): a parked pass
+// (64 x (BN + 4) fp32) and two 16 KB residual buffers. Pass 0's residual is DMA'd during the main loop's
+// last taps into the halo buffer the last channel block does not read, so the layout depends on the
+// parity of the channel-block count.
+constexpr int PK_BYTES = 64 * (BN + 4) * 4;  // 33,792
+constexpr int RES_BYTES = 64 * BN * 2;       // 16,384: 64 pixels x 128 bf16
+constexpr int RING_END = 2 * HBYTES + NB * BBYTES;
+static_assert(HBYTES + PK_BYTES + RES_BYTES <= RING_END, "epilogue plan, even channel blocks");
+static_assert(HBYTES + RES_BYTES + PK_BYTES <= RING_END, "epilogue plan, odd channel blocks");
+static_assert(RES_BYTES <= HBYTES, "pass-0 residual in the free halo buffer");
+__device__ __forceinline__ int res_off(int parity, int p) {  // residual buffer of pass p
+  return ((p & 1) == 0) ? (parity ? HBYTES : 0) : (parity ? 0 : HBYTES + PK_BYTES);
+}
+__device__ __forceinline__ int park_off(int parity) { return parity ? HBYTES + RES_BYTES : HBYTES; }
 }  // namespace halo
+
+// The halo conv's epilogue for bf16 outputs without emb / activation (every VAE ResnetBlock conv):
+// out = (acc + bias) + residual, rounded to bf16, in four passes of 64 tile rows. Per pass: the
+// accumulators of fragment row p are parked in LDS; the residual rows of the pass are already in LDS
+// (LDS-DMA issued one pass ahead, so its HBM latency overlaps the previous pass instead of stalling
+// every chunk); each thread keeps the bias of its 8 channels in registers and handles 2 chunks
+// (16-byte LDS reads, residual read, one 16-byte store each). Arithmetic and rounding are epilogue_vec's,
+// so outputs are bit-identical to it. Fused GroupNorm statistics (a.gn_part) keep the canonical order:
+// pass p is 16-row group p of every 64-row block (one wave row), summed by a column scan of the stored
+// values, and ((g0 + g1) + g2) + g3 at the end.
+// The residual rows of epilogue pass p (64 pixels x 128 channels, 16 KB) by LDS-DMA: this wave's pieces
+// q = wave, wave + 8; lane i of piece q brings pass row 4q + i / 16 (wave row (4q + i / 16) / 16, pixel
+// p * 16 + (4q + i / 16) % 16 of it), chunk i % 16. Offsets are recomputed at each use (not kept live).
+__device__ __forceinline__ void halo_res_dma(__amdgpu_buffer_rsrc_t rsr, char* dst, int base, int W, int res_ld,
+                                             int wave, int lane, int p) {
+  int l = lane;
+  asm volatile("" : "+v"(l));  // keep the offsets here, not hoisted into the main loop's live set
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int pr = 4 * (wave + 8 * k) + (l >> 4);
+    const unsigned vo = (unsigned)(base + (pr >> 4) * W + (pr & 15)) * (unsigned)(res_ld * 2) + (unsigned)((l & 15) * 16);
+    dma16(rsr, dst + (wave + 8 * k) * 1024, vo, p * 16 * res_ld * 2);
+  }
+}
+
+__device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const ConvArgs& a, int n0, int wm, int wn,
+                                              int lane, int tid, char* lds, int base, int W, int parity,
+                                              __amdgpu_buffer_rsrc_t rsr, int wave) {
+  using namespace halo;
+  constexpr int SDW = BN + 4;
+  // laundered: every address below is derived after the main loop (hoisted, they would sit in the
+  // 128-VGPR main loop's live set and spill)
+  asm volatile("" : "+v"(tid));
+  lane = tid & 63;
+  const int lr = lane & 15, lq = lane >> 4;
+  float* const L = reinterpret_cast<float*>(lds + park_off(parity));
+  const bool has_res = a.res != nullptr;
+  const bool st = a.gn_part != nullptr;
+  const int cc = tid & 15;  // this thread's 8 channels n0 + 8 cc (NT % 16 == 0: the same in every chunk)
+  const int nn = n0 + cc * 8;
+  float bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+  if (a.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + nn), b1 = *reinterpret_cast<const float4*>(a.bias + nn + 4);
+    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w; bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+  }
+  float sg[4], qg[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    __syncthreads();  // p = 0: the main loop's LDS reads are done; else: the previous pass's readers are
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) L[(wm * 16 + lq * 4 + r) * SDW + wn * 64 + j * 16 + lr] = acc[p][j][r];
+    if (has_res) {  // this wave's residual pieces of pass p (younger: the 2 stores of pass p - 1)
+      if (p == 0) wait_vm<0>(); else wait_vm<2>();
+    }
+    __syncthreads();
+    if (has_res && p + 1 < 4)  // the next pass's residual into the buffer pass p - 1 read
+      halo_res_dma(rsr, lds + res_off(parity, p + 1), base, W, a.res_ld, wave, lane, p + 1);
+    const char* R = lds + res_off(parity, p);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pr = (tid >> 4) + 32 * k;  // pass row: wave row pr / 16, row p * 16 + pr % 16 of it
+      const long m = base + (pr >> 4) * W + p * 16 + (pr & 15);
+      const float4 x0 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8 + 4);
+      float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias[e];
+      if (has_res) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + pr * 256 + cc * 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+      }
+      bf16x8 ov;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.out) + m * a.out_ld + nn) = ov;
+      if (st) {
+        *reinterpret_cast<float4*>(L + pr * SDW + cc * 8) = make_float4((float)ov[0], (float)ov[1], (float)ov[2], (float)ov[3]);
+        *reinterpret_cast<float4*>(L + pr * SDW + cc * 8 + 4) = make_float4((float)ov[4], (float)ov[5], (float)ov[6], (float)ov[7]);
+      }
+    }
+    if (st) {  // column scan: thread (wave row b, channel j), the 16 rows of group p, in row order
+      __syncthreads();
+      const int b = tid >> 7, j = tid & 127;
+      const float* col = L + (b * 16) * SDW + j;
+      float y[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) y[r] = col[r * SDW];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s1 += y[r]; s2 = fmaf(y[r], y[r], s2); }
+      sg[p] = s1;
+      qg[p] = s2;
+    }
+  }
+  if (st) {
+    const int b = tid >> 7, j = tid & 127;
+    float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + base + b * W) / 64) * a.cout + n0 + j) * 2;
+    pp[0] = ((sg[0] + sg[1]) + sg[2]) + sg[3];
+    pp[1] = ((qg[0] + qg[1]) + qg[2]) + qg[3];
+    if (tid == 0 && base == 0 && n0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
+  }
+}
 
 #ifdef RDEIC_HALO_STAMPS
 // diagnostic build only (tools/halo_stamps.hip): per-block shader-clock stamps, 8 u64 per block,
@@ -1290,7 +1412,8 @@ __device__ unsigned long long* g_halo_stamps;
 #define HALO_STAMP(k) do {} while (0)
 #endif
 
-template <bool GN>
+// FE: the fast epilogue (halo_epilogue: bf16 out, no emb / activation), else epilogue_vec
+template <bool GN, bool FE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3x3_halo_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
                                                                unsigned bytesw) {
   using namespace halo;
@@ -1348,6 +1471,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         hvo[k] = (unsigned)((img * H + iy) * W + ix) * (unsigned)(a.ld0 * 2) + (unsigned)((ph ^ sw(sl)) * 16);
     }
   }
+  // residual pieces of the epilogue (halo_epilogue): this wave's pieces q = wave, wave + 8 of every pass;
+  // lane i of piece q brings pass row 4q + i / 16 (wave row (4q + i / 16) / 16), chunk i % 16
+  const bool res_dma = FE && a.res != nullptr;
+  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(res_dma ? a.res : a.in0), (short)0, res_dma ? (int)((long)(img * H + H) * W * a.res_ld * 2) : 0, 0x00020000);
+  const int parity = (cin >> 5) & 1;
   // weight rows of this wave: n = 16 wave + lane / 4, chunk lane % 4
   unsigned bvo;
   {
@@ -1440,6 +1569,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         if (more) wait_vm<5>(); else wait_vm<1>();
       } else if (t < 8 || more) {
         wait_vm<1>();
+      } else if (res_dma) {
+        wait_vm<2>();  // younger: the epilogue's pass-0 residual pieces (issued at tap 7)
       } else {
         wait_vm<0>();
       }
@@ -1452,6 +1583,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         dma16(rsw, bbuf + ((t + 2) % NB) * BBYTES + wave * 1024, bvo, ((t + 2 - 9) * cin + (cb + 1) * 32) * 2);
       }
       if (t == 0 && more) issue_halo(cb + 1);
+      if (t == 7 && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
+        halo_res_dma(rsr, lds + halo::res_off(parity, 0), (img * H + oy0) * W + ox0, W, a.res_ld, wave, lane, 0);
       const char* bb = bbuf + (t % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
       const int ky = t / 3, kx = t - (t / 3) * 3;
       bf16x8 bfv[4];
@@ -1472,8 +1605,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
   }
   HALO_STAMP(2);
-  epilogue_vec<TR * TC, BN, 4, 2, NT, 2>(acc, a, 0, n0, wm, wn, lane, tid, lds,
-                                         Rows{(img * H + oy0) * W + ox0, W});
+  if constexpr (FE)
+    halo_epilogue(acc, a, n0, wm, wn, lane, tid, lds, (img * H + oy0) * W + ox0, W, parity, rsr, wave);
+  else
+    epilogue_vec<TR * TC, BN, 4, 2, NT, 2>(acc, a, 0, n0, wm, wn, lane, tid, lds,
+                                           Rows{(img * H + oy0) * W + ox0, W});
   HALO_STAMP(3);
 }
 
@@ -1512,10 +1648,15 @@ int launch_halo(const rdeic_conv_desc* d, ConvArgs a, hipStream_t s, bool* fused
     const int tx = d->w / TC, ty = d->h / TR;
     const long tiles = (long)e.n * ty * tx * (d->cout / BN);
     rdeic_count_launch(RDEIC_COUNT_HALO_CONV);
-    if (e.gn_ab)
-      hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
+    const bool fe = !e.out_f32 && !e.emb && e.act == 0;
+    if (e.gn_ab && fe)
+      hipLaunchKernelGGL((conv3x3_halo_kernel<true, true>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
+    else if (e.gn_ab)
+      hipLaunchKernelGGL((conv3x3_halo_kernel<true, false>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
+    else if (fe)
+      hipLaunchKernelGGL((conv3x3_halo_kernel<false, true>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
     else
-      hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
+      hipLaunchKernelGGL((conv3x3_halo_kernel<false, false>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
     const int rc = launch_status();
     if (rc != RDEIC_OK) return rc;
   }
