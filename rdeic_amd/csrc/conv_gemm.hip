@@ -1446,11 +1446,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;  // wave = (output row, 64-channel half)
 
-  if constexpr (GN) {  // the image's (a, b) table, before any DMA is in flight (plain vmcnt use)
-    const float* src = a.gn_ab + (long)img * cin * 2;
-    for (int i = tid; i < cin * 2; i += NT) abl[i] = src[i];
-  }
-
   const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)bytes0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)a.weight, (short)0, (int)bytesw, 0x00020000);
 
@@ -1544,12 +1539,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (GN) __syncthreads();  // the affine table is in LDS (its global loads have drained)
+  // prologue: the image's GroupNorm (a, b) table (cin x 8 bytes, <= 4 KB) comes by LDS-DMA together with
+  // the first halo and weight slices, so their latencies overlap. Each wave issues ONE table piece (waves
+  // past the table's pieces repeat piece 0: same bytes to the same slots), keeping vmcnt uniform.
+  if constexpr (GN) {
+    const int tbytes = cin * 8, tp = wave < (tbytes + 1023) / 1024 ? wave : 0;
+    const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.gn_ab + (long)img * cin * 2), (short)0, tbytes, 0x00020000);
+    dma16(rst, reinterpret_cast<char*>(abl) + tp * 1024, (unsigned)(tp * 1024 + lane * 16), 0);
+  }
   issue_halo(0);
   issue_b(0);
   issue_b(1);
-  wait_vm<2>();  // this wave's halo pieces
-  if constexpr (GN) transform(0);
+  wait_vm<2>();  // the table piece and this wave's halo pieces
+  if constexpr (GN) {
+    __syncthreads();  // every wave's table piece has landed
+    transform(0);
+  }
 
   HALO_STAMP(1);
   const int lr = lane & 15, lq = lane >> 4;
