@@ -1304,16 +1304,17 @@ __device__ __forceinline__ int park_off(int parity) { return parity ? HBYTES + R
 // values, and ((g0 + g1) + g2) + g3 at the end.
 // The residual rows of epilogue pass p (64 pixels x 128 channels, 16 KB) by LDS-DMA: this wave's pieces
 // q = wave, wave + 8; lane i of piece q brings pass row 4q + i / 16 (wave row (4q + i / 16) / 16, pixel
-// p * 16 + (4q + i / 16) % 16 of it), chunk i % 16. Offsets are recomputed at each use (not kept live).
+// p * 16 + (4q + i / 16) % 16 of it), channels n0 + 8 (i % 16) .. + 7. Offsets are recomputed at each use
+// (not kept live).
 __device__ __forceinline__ void halo_res_dma(__amdgpu_buffer_rsrc_t rsr, char* dst, int base, int W, int res_ld,
-                                             int wave, int lane, int p) {
+                                             int n0, int wave, int lane, int p) {
   int l = lane;
   asm volatile("" : "+v"(l));  // keep the offsets here, not hoisted into the main loop's live set
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int pr = 4 * (wave + 8 * k) + (l >> 4);
     const unsigned vo = (unsigned)(base + (pr >> 4) * W + (pr & 15)) * (unsigned)(res_ld * 2) + (unsigned)((l & 15) * 16);
-    dma16(rsr, dst + (wave + 8 * k) * 1024, vo, p * 16 * res_ld * 2);
+    dma16(rsr, dst + (wave + 8 * k) * 1024, vo, p * 16 * res_ld * 2 + n0 * 2);
   }
 }
 
@@ -1352,7 +1353,7 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
     }
     __syncthreads();
     if (has_res && p + 1 < 4)  // the next pass's residual into the buffer pass p - 1 read
-      halo_res_dma(rsr, lds + res_off(parity, p + 1), base, W, a.res_ld, wave, lane, p + 1);
+      halo_res_dma(rsr, lds + res_off(parity, p + 1), base, W, a.res_ld, n0, wave, lane, p + 1);
     const char* R = lds + res_off(parity, p);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -1410,6 +1411,11 @@ __device__ unsigned long long* g_halo_stamps;
   } while (0)
 #else
 #define HALO_STAMP(k) do {} while (0)
+#endif
+// diagnostic build only: RDEIC_HALO_DIAG bits remove one mechanism of the main loop (results wrong,
+// timing tells what bounds it): 1 per-tap DMA waits, 2 per-tap barriers, 4 MFMAs, 8 GroupNorm transform
+#ifndef RDEIC_HALO_DIAG
+#define RDEIC_HALO_DIAG 0
 #endif
 
 // FE: the fast epilogue (halo_epilogue: bf16 out, no emb / activation), else epilogue_vec
@@ -1571,7 +1577,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int t = 0; t < 9; ++t) {
       // this tap's weights (and at tap 2 the next halo); younger ops allowed in flight: the next tap's
       // weights and, at tap 1, the next halo's 4 pieces issued at tap 0
-      if (t == 1) {
+      if (RDEIC_HALO_DIAG & 1) {
+        if (t == 8 && !more) wait_vm<0>();
+      } else if (t == 1) {
         if (more) wait_vm<5>(); else wait_vm<1>();
       } else if (t < 8 || more) {
         wait_vm<1>();
@@ -1580,9 +1588,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       } else {
         wait_vm<0>();
       }
-      if constexpr (GN)
+      if constexpr (GN && !(RDEIC_HALO_DIAG & 8))
         if (t == 2 && more) transform(cb + 1);  // own pieces landed (waited above); read from (cb + 1, 0)
-      __builtin_amdgcn_s_barrier();
+      if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (t + 2 < 9) {
         dma16(rsw, bbuf + ((t + 2) % NB) * BBYTES + wave * 1024, bvo, ((t + 2) * cin + cb * 32) * 2);
       } else if (more) {
@@ -1590,7 +1598,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       }
       if (t == 0 && more) issue_halo(cb + 1);
       if (t == 7 && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
-        halo_res_dma(rsr, lds + halo::res_off(parity, 0), (img * H + oy0) * W + ox0, W, a.res_ld, wave, lane, 0);
+        halo_res_dma(rsr, lds + halo::res_off(parity, 0), (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
       const char* bb = bbuf + (t % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
       const int ky = t / 3, kx = t - (t / 3) * 3;
       bf16x8 bfv[4];
@@ -1606,7 +1614,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int i = 0; i < 4; ++i) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          if (RDEIC_HALO_DIAG & 4)
+            asm volatile("" ::"v"(af), "v"(bfv[j]));
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
   }
