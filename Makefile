@@ -2,14 +2,14 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
 ARCH ?= gfx950
-BUILD := build
-LIBDIR := rdeic_amd/lib
+BUILD ?= build
+LIBDIR ?= rdeic_amd/lib
 LIB := $(LIBDIR)/librdeic_hip.so
 HIP_SRCS := $(wildcard rdeic_amd/csrc/*.hip)
 CPP_SRCS := $(wildcard rdeic_amd/csrc/*.cpp)
 HIP_OBJS := $(patsubst rdeic_amd/csrc/%.hip,$(BUILD)/%.hip.o,$(HIP_SRCS))
 CPP_OBJS := $(patsubst rdeic_amd/csrc/%.cpp,$(BUILD)/%.cpp.o,$(CPP_SRCS))
-HIPFLAGS := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-variable -Wno-unused-but-set-variable
+HIPFLAGS := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-variable -Wno-unused-but-set-variable $(EXTRA_HIPFLAGS)
 CXXFLAGS := -O3 -fPIC -std=c++17 -Wall -pthread
 
 all: $(LIB) oracle

@@ -1418,8 +1418,9 @@ __device__ unsigned long long* g_halo_stamps;
 #define RDEIC_HALO_DIAG 0
 #endif
 
+// GN: 0 plain conv, 1 GroupNorm affine on the input, 2 affine + SiLU (compile-time: no per-element branch);
 // FE: the fast epilogue (halo_epilogue: bf16 out, no emb / activation), else epilogue_vec
-template <bool GN, bool FE>
+template <int GN, bool FE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3x3_halo_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
                                                                unsigned bytesw) {
   using namespace halo;
@@ -1526,7 +1527,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
           const float4 ab = ab4[q];  // (a, b) of channels 2q, 2q + 1 of the chunk
           float x0 = __builtin_fmaf((float)v[k - k0][2 * q], ab.x, ab.y);
           float x1 = __builtin_fmaf((float)v[k - k0][2 * q + 1], ab.z, ab.w);
-          if (a.gn_silu) {
+          if constexpr (GN == 2) {
             x0 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x0));
             x1 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x1));
           }
@@ -1548,7 +1549,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   // prologue: the image's GroupNorm (a, b) table (cin x 8 bytes, <= 4 KB) comes by LDS-DMA together with
   // the first halo and weight slices, so their latencies overlap. Each wave issues ONE table piece (waves
   // past the table's pieces repeat piece 0: same bytes to the same slots), keeping vmcnt uniform.
-  if constexpr (GN) {
+  if constexpr (GN != 0) {
     const int tbytes = cin * 8, tp = wave < (tbytes + 1023) / 1024 ? wave : 0;
     const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.gn_ab + (long)img * cin * 2), (short)0, tbytes, 0x00020000);
@@ -1558,7 +1559,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   issue_b(0);
   issue_b(1);
   wait_vm<2>();  // the table piece and this wave's halo pieces
-  if constexpr (GN) {
+  if constexpr (GN != 0) {
     __syncthreads();  // every wave's table piece has landed
     transform(0);
   }
@@ -1588,7 +1589,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       } else {
         wait_vm<0>();
       }
-      if constexpr (GN && !(RDEIC_HALO_DIAG & 8))
+      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
         if (t == 2 && more) transform(cb + 1);  // own pieces landed (waited above); read from (cb + 1, 0)
       if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (t + 2 < 9) {
@@ -1668,14 +1669,14 @@ int launch_halo(const rdeic_conv_desc* d, ConvArgs a, hipStream_t s, bool* fused
     const long tiles = (long)e.n * ty * tx * (d->cout / BN);
     rdeic_count_launch(RDEIC_COUNT_HALO_CONV);
     const bool fe = !e.out_f32 && !e.emb && e.act == 0;
-    if (e.gn_ab && fe)
-      hipLaunchKernelGGL((conv3x3_halo_kernel<true, true>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
-    else if (e.gn_ab)
-      hipLaunchKernelGGL((conv3x3_halo_kernel<true, false>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
-    else if (fe)
-      hipLaunchKernelGGL((conv3x3_halo_kernel<false, true>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
-    else
-      hipLaunchKernelGGL((conv3x3_halo_kernel<false, false>), dim3((unsigned)tiles), dim3(NT), LDS, s, e, tx, ty, b0, bw);
+    const int gm = e.gn_ab ? (e.gn_silu ? 2 : 1) : 0;
+    const dim3 g((unsigned)tiles), b(NT);
+    if (gm == 2 && fe) hipLaunchKernelGGL((conv3x3_halo_kernel<2, true>), g, b, LDS, s, e, tx, ty, b0, bw);
+    else if (gm == 2) hipLaunchKernelGGL((conv3x3_halo_kernel<2, false>), g, b, LDS, s, e, tx, ty, b0, bw);
+    else if (gm == 1 && fe) hipLaunchKernelGGL((conv3x3_halo_kernel<1, true>), g, b, LDS, s, e, tx, ty, b0, bw);
+    else if (gm == 1) hipLaunchKernelGGL((conv3x3_halo_kernel<1, false>), g, b, LDS, s, e, tx, ty, b0, bw);
+    else if (fe) hipLaunchKernelGGL((conv3x3_halo_kernel<0, true>), g, b, LDS, s, e, tx, ty, b0, bw);
+    else hipLaunchKernelGGL((conv3x3_halo_kernel<0, false>), g, b, LDS, s, e, tx, ty, b0, bw);
     const int rc = launch_status();
     if (rc != RDEIC_OK) return rc;
   }
