@@ -41,3 +41,7 @@ $(BUILD)/attention.hip.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form=1
 
 # parity-sensitive scalar kernels: no fma contraction anywhere in these TUs (headers included)
 $(BUILD)/elementwise.hip.o $(BUILD)/entropy.hip.o: HIPFLAGS += -ffp-contract=off
+
+# conv kernels: no SLP vectorisation (packed-f32 VALU beside MFMAs is an anti-lever on gfx950,
+# MI355X_MICROARCH.md constants table; measured r04 on the halo conv: -1 to -2% time)
+$(BUILD)/conv_gemm.hip.o: HIPFLAGS += -fno-slp-vectorize

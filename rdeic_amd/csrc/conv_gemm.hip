@@ -1508,35 +1508,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (p >= 0 && hvo[k] != kOOB) hinfo |= 1u << k;
     hinfo |= (unsigned)((lane & 3) ^ sw(sl)) << (4 + 2 * k);
   }
-  auto transform = [&](int cb) {
-    char* hb = hbuf + (cb & 1) * HBYTES + lane * 16;
+  // piece k of this wave's halo pieces (one 16-byte chunk per lane), transformed in place
+  auto transform_piece = [&](int cb, int k) {
+    if (!(hinfo & (1u << k))) return;
+    char* hb = hbuf + (cb & 1) * HBYTES + lane * 16 + hpo[k];
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(hb);
+    const int ch = (hinfo >> (4 + 2 * k)) & 3;
+    const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
+    const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];  // (a, b) of the chunk's 8 channels
+    const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+    const float bv[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+    bf16x8 o;
 #pragma unroll
-    for (int k0 = 0; k0 < 4; k0 += 2) {  // two chunks in flight at a time (register budget)
-      bf16x8 v[2];
-#pragma unroll
-      for (int k = k0; k < k0 + 2; ++k)
-        if (hinfo & (1u << k)) v[k - k0] = *reinterpret_cast<const bf16x8*>(hb + hpo[k]);
-#pragma unroll
-      for (int k = k0; k < k0 + 2; ++k) {
-        if (!(hinfo & (1u << k))) continue;
-        const int ch = (hinfo >> (4 + 2 * k)) & 3;
-        const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
-        bf16x8 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 ab = ab4[q];  // (a, b) of channels 2q, 2q + 1 of the chunk
-          float x0 = __builtin_fmaf((float)v[k - k0][2 * q], ab.x, ab.y);
-          float x1 = __builtin_fmaf((float)v[k - k0][2 * q + 1], ab.z, ab.w);
-          if constexpr (GN == 2) {
-            x0 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x0));
-            x1 *= __builtin_amdgcn_rcpf(1.0f + __expf(-x1));
-          }
-          o[2 * q] = (bf16)x0;
-          o[2 * q + 1] = (bf16)x1;
-        }
-        *reinterpret_cast<bf16x8*>(hb + hpo[k]) = o;
-      }
+    for (int e = 0; e < 8; ++e) {
+      float x = __builtin_fmaf((float)v[e], av[e], bv[e]);
+      if constexpr (GN == 2) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+      o[e] = (bf16)x;
     }
+    *reinterpret_cast<bf16x8*>(hb) = o;
+  };
+  auto transform = [&](int cb) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) transform_piece(cb, k);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
   };
 
@@ -1589,8 +1582,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       } else {
         wait_vm<0>();
       }
+      // the next block's halo (own pieces landed at tap 2's wait) is transformed one piece per tap over
+      // taps 2..5, spreading its VALU between the MFMA segments; it is read from tap (cb + 1, 0) on
       if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
-        if (t == 2 && more) transform(cb + 1);  // own pieces landed (waited above); read from (cb + 1, 0)
+        if (t >= 2 && t < 6 && more) {
+          transform_piece(cb + 1, t - 2);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before this tap's barrier
+        }
       if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (t + 2 < 9) {
         dma16(rsw, bbuf + ((t + 2) % NB) * BBYTES + wave * 1024, bvo, ((t + 2) * cin + cb * 32) * 2);
