@@ -145,6 +145,7 @@ def main():
         ops.call("rdeic_image_mse", imgs.data_ptr(), out.data_ptr(), B, S * S * 3, mse.data_ptr(), ops.stream_ptr())
         m = mse.cpu().numpy()
         _, ms = quality.ssim_ms_ssim(out, imgs)  # on the device (rdeic_image_ssim)
+        sess._last_out = out  # the step's u8 images (bf16-vs-fp32 pixel PSNR of the fp32 leg)
         return torch.tensor([[len(b) * 8.0 / (S * S), float(len(b)),
                               10 * math.log10(255.0 ** 2 / max(float(v), 1e-10)), float(v), float(q), 1.0, float(rank)]
                              for b, v, q in zip(bodies, m, ms)], dtype=torch.float32)
@@ -218,11 +219,15 @@ def main():
             prof = dict(prof, _wall_s=rf_elapsed)
         elapsed = parallel.max_over_ranks(elapsed, dev)
         mrows = metrics.cpu().numpy()
-        results.append({"target_bpp": target, "rate_gain": rate_gain, "elapsed": elapsed, "prof": prof,
+        last_out = sessions[(args.steps - 1) % nsess]._last_out
+        results.append({"target_bpp": target, "rate_gain": rate_gain, "elapsed": elapsed, "prof": prof, "out": last_out,
                         "mean_bpp": float(mrows[:, 0].mean()), "mean_psnr_db": float(mrows[:, 2].mean()),
                         "mean_ms_ssim": float(mrows[:, 4].mean()),
                         "images": int(mrows.shape[0]), "rows": rows_by_step[-1].numpy()})
         del sessions
+        for rr in results:
+            if rr is not results[main_i]:
+                rr.pop("out", None)
     fp32_leg = None
     if world == 1 and args.dtype == "bf16" and args.fp32_steps > 0 and not args.bpp_sweep:
         log(f"fp32 parity mode: 1 warm-up + {args.fp32_steps} timed steps on one session, same images")
@@ -241,6 +246,8 @@ def main():
         el32 = time.perf_counter() - t0
         r32 = rows32.numpy()
         r16 = results[main_i]["rows"]
+        d = results[main_i]["out"].double() - m32._last_out.double()
+        px_psnr = 10 * math.log10(255.0 ** 2 / max(float(d.pow(2).mean()), 1e-12))
         fp32_leg = {
             "dtype": "fp32", "path": "bitstream-parity (fp32 convs on v_mfma_f32_16x16x4f32; file bodies byte-equal "
                                      "to the oracle's, pixels within 1e-3 abs: tests/test_config2_gpu.py)",
@@ -251,7 +258,9 @@ def main():
                 "mean_bpp_rel": round(float((r16[:, 0].mean() - r32[:, 0].mean()) / r32[:, 0].mean()), 5),
                 "max_image_bpp_rel": round(float(np.abs((r16[:, 0] - r32[:, 0]) / r32[:, 0]).max()), 5),
                 "mean_psnr_db": round(float(r16[:, 2].mean() - r32[:, 2].mean()), 4),
-                "mean_ms_ssim": round(float(r16[:, 4].mean() - r32[:, 4].mean()), 5)}}
+                "mean_ms_ssim": round(float(r16[:, 4].mean() - r32[:, 4].mean()), 5)},
+            # the decoded u8 pixels of the two modes against each other (each codes its own bitstream)
+            "bf16_vs_fp32_pixel_psnr_db": round(px_psnr, 2)}
         del m32
     parallel.finish()  # every rank leaves the group before rank 0's CPU-baseline leg
     if rank != 0:

@@ -1582,13 +1582,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       } else {
         wait_vm<0>();
       }
-      // the next block's halo (own pieces landed at tap 2's wait) is transformed one piece per tap over
-      // taps 2..5, spreading its VALU between the MFMA segments; it is read from tap (cb + 1, 0) on
-      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
-        if (t >= 2 && t < 6 && more) {
-          transform_piece(cb + 1, t - 2);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before this tap's barrier
-        }
       if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (t + 2 < 9) {
         dma16(rsw, bbuf + ((t + 2) % NB) * BBYTES + wave * 1024, bvo, ((t + 2) * cin + cb * 32) * 2);
@@ -1620,6 +1613,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
         }
       }
+      // the next block's halo (own pieces landed at tap 2's wait) is transformed one piece per tap over
+      // taps 2..5, AFTER this tap's MFMAs are issued, so its VALU runs beside the matrix pipe instead of
+      // delaying the next barrier; the block reads it from its tap 0 on (several barriers later)
+      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
+        if (t >= 2 && t < 6 && more) {
+          transform_piece(cb + 1, t - 2);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier
+        }
     }
   }
   HALO_STAMP(2);
