@@ -121,6 +121,9 @@ int rdeic_set_conv_path(int32_t path);
  * key 8: head-dim-512 attention: 2 wave pairs splitting d over 32 queries (default, for L >= 4096:
  *        a per-image rule, so outputs stay batch-invariant), 1 one wave per 16 queries everywhere
  *        (fp32-rounding-level differences);
+ * key 9: the halo conv's 8-row form (one 1024-thread block per CU, 8-slot weight ring) where the
+ *        output height is a multiple of 8 and the epilogue is bf16 without emb / activation: 1 on
+ *        (default), 0 the 4-row form everywhere (bit-identical outputs);
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way
  * (keys 0-5; 6 and 8 change fp32 rounding only). */
 int rdeic_set_conv_option(int32_t key, int32_t value);

@@ -1302,33 +1302,44 @@ __device__ __forceinline__ int park_off(int parity) { return parity ? HBYTES + R
 // so outputs are bit-identical to it. Fused GroupNorm statistics (a.gn_part) keep the canonical order:
 // pass p is 16-row group p of every 64-row block (one wave row), summed by a column scan of the stored
 // values, and ((g0 + g1) + g2) + g3 at the end.
-// The residual rows of epilogue pass p (64 pixels x 128 channels, 16 KB) by LDS-DMA: this wave's pieces
-// q = wave, wave + 8; lane i of piece q brings pass row 4q + i / 16 (wave row (4q + i / 16) / 16, pixel
+// The residual rows of epilogue pass p (NW x 8 pixels x 128 channels) by LDS-DMA: this wave's pieces
+// q = wave, wave + NW; lane i of piece q brings pass row 4q + i / 16 (wave row (4q + i / 16) / 16, pixel
 // p * 16 + (4q + i / 16) % 16 of it), channels n0 + 8 (i % 16) .. + 7. Offsets are recomputed at each use
 // (not kept live).
+template <int NW>
 __device__ __forceinline__ void halo_res_dma(__amdgpu_buffer_rsrc_t rsr, char* dst, int base, int W, int res_ld,
                                              int n0, int wave, int lane, int p) {
   int l = lane;
   asm volatile("" : "+v"(l));  // keep the offsets here, not hoisted into the main loop's live set
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const int pr = 4 * (wave + 8 * k) + (l >> 4);
+    const int pr = 4 * (wave + NW * k) + (l >> 4);
     const unsigned vo = (unsigned)(base + (pr >> 4) * W + (pr & 15)) * (unsigned)(res_ld * 2) + (unsigned)((l & 15) * 16);
-    dma16(rsr, dst + (wave + 8 * k) * 1024, vo, p * 16 * res_ld * 2 + n0 * 2);
+    dma16(rsr, dst + (wave + NW * k) * 1024, vo, p * 16 * res_ld * 2 + n0 * 2);
   }
 }
 
+// The halo convs' epilogue for bf16 outputs without emb / activation (every VAE ResnetBlock conv):
+// out = (acc + bias) + residual, rounded to bf16, in four passes (one 16-row fragment per wave row, NW x 8
+// tile rows). Per pass: the accumulators of fragment row p are parked in LDS (park); the residual rows of
+// the pass are already in LDS (r0 / r1 alternate; LDS-DMA issued one pass ahead, so its latency overlaps
+// the previous pass instead of stalling every chunk; pass 0's is issued by the caller during its last
+// taps); each thread keeps the bias of its 8 channels in registers and handles 2 chunks (16-byte LDS reads,
+// residual read, one 16-byte store each). Arithmetic and rounding are epilogue_vec's, so outputs are
+// bit-identical to it. Fused GroupNorm statistics (a.gn_part) keep the canonical order: pass p is 16-row
+// group p of every 64-row block (one wave row), summed by a column scan of the stored values, and
+// ((g0 + g1) + g2) + g3 at the end.
+template <int NW>
 __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const ConvArgs& a, int n0, int wm, int wn,
-                                              int lane, int tid, char* lds, int base, int W, int parity,
+                                              int tid, char* lds, int base, int W, int park, int r0, int r1,
                                               __amdgpu_buffer_rsrc_t rsr, int wave) {
-  using namespace halo;
-  constexpr int SDW = BN + 4;
+  constexpr int BN = 128, SDW = BN + 4, NT = NW * 64;
   // laundered: every address below is derived after the main loop (hoisted, they would sit in the
   // 128-VGPR main loop's live set and spill)
   asm volatile("" : "+v"(tid));
-  lane = tid & 63;
+  const int lane = tid & 63;
   const int lr = lane & 15, lq = lane >> 4;
-  float* const L = reinterpret_cast<float*>(lds + park_off(parity));
+  float* const L = reinterpret_cast<float*>(lds + park);
   const bool has_res = a.res != nullptr;
   const bool st = a.gn_part != nullptr;
   const int cc = tid & 15;  // this thread's 8 channels n0 + 8 cc (NT % 16 == 0: the same in every chunk)
@@ -1353,11 +1364,11 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
     }
     __syncthreads();
     if (has_res && p + 1 < 4)  // the next pass's residual into the buffer pass p - 1 read
-      halo_res_dma(rsr, lds + res_off(parity, p + 1), base, W, a.res_ld, n0, wave, lane, p + 1);
-    const char* R = lds + res_off(parity, p);
+      halo_res_dma<NW>(rsr, lds + ((p + 1) & 1 ? r1 : r0), base, W, a.res_ld, n0, wave, lane, p + 1);
+    const char* R = lds + (p & 1 ? r1 : r0);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const int pr = (tid >> 4) + 32 * k;  // pass row: wave row pr / 16, row p * 16 + pr % 16 of it
+      const int pr = (tid >> 4) + (NT / 16) * k;  // pass row: wave row pr / 16, row p * 16 + pr % 16 of it
       const long m = base + (pr >> 4) * W + p * 16 + (pr & 15);
       const float4 x0 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8);
       const float4 x1 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8 + 4);
@@ -1590,7 +1601,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       }
       if (t == 0 && more) issue_halo(cb + 1);
       if (t == 7 && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
-        halo_res_dma(rsr, lds + halo::res_off(parity, 0), (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
+        halo_res_dma<NW>(rsr, lds + halo::res_off(parity, 0), (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
       const char* bb = bbuf + (t % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
       const int ky = t / 3, kx = t - (t / 3) * 3;
       bf16x8 bfv[4];
@@ -1625,12 +1636,240 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   }
   HALO_STAMP(2);
   if constexpr (FE)
-    halo_epilogue(acc, a, n0, wm, wn, lane, tid, lds, (img * H + oy0) * W + ox0, W, parity, rsr, wave);
+    halo_epilogue<NW>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(parity),
+                      res_off(parity, 0), res_off(parity, 1), rsr, wave);
   else
     epilogue_vec<TR * TC, BN, 4, 2, NT, 2>(acc, a, 0, n0, wm, wn, lane, tid, lds,
                                            Rows{(img * H + oy0) * W + ox0, W});
   HALO_STAMP(3);
 }
+
+// ============================================================================================
+// The 8-row halo conv (r04): one 1024-thread block per CU computes 8 x 64 output pixels x 128 channels
+// (16 waves: 8 output rows x 2 channel halves of 64, the same 64 x 64 wave tile as conv3x3_halo_kernel).
+// Against the 4-row kernel (two 512-thread blocks per CU) it trades the second co-resident block for
+// depth: the whole 160 KB of LDS holds a 10 x 66-pixel halo double buffer (1.29 halo pixels per output
+// pixel instead of 1.55) and an 8-slot weight ring fed 6 taps ahead (the 4-row kernel's 3-slot ring,
+// 2 taps ahead, left the main loop waiting on ~1.1 us LDS-DMA landings, tools/halo_stamps.hip, r04).
+// Roles are split so every wave's vmcnt counts only its own stream: waves 0..7 stream the weight slices
+// (1 KB = 16 rows each), waves 8..15 the halo pieces (6 each, duplicates for the 42 pieces) and the
+// GroupNorm table, and transform the pieces they loaded (affine + SiLU in place). Same MFMA order as
+// the 4-row kernel (channel block major, tap minor), so both give bit-identical outputs.
+// ============================================================================================
+namespace halo8 {
+constexpr int TR = 8, TC = 64;
+constexpr int HR = TR + 2, HC = TC + 2;            // 10 x 66 halo pixels
+constexpr int HPIX = HR * HC;                      // 660
+constexpr int NPIECE = (HPIX * 4 + 63) / 64;       // 42 pieces of 1 KB
+constexpr int HBYTES = NPIECE * 1024;              // 43,008
+constexpr int BN = 128, NW = 16, NT = NW * 64;
+constexpr int BBYTES = BN * 64;                    // one tap's 32-channel weight slice
+constexpr int NB = 8, LEAD = 6;                    // weight ring: slice u + LEAD issued at tap u
+constexpr int PPW = 6;                             // halo pieces per halo wave (8 waves x 6 >= 42)
+constexpr int AB_MAX = 512;
+constexpr int TABLE = 2 * HBYTES + NB * BBYTES;    // 151,552
+constexpr int LDS = TABLE + AB_MAX * 8;            // 155,648
+static_assert(LDS <= 160 * 1024, "one block per CU");
+static_assert(NB >= LEAD + 1, "a slot is reused only after every wave passed the barrier of its last reader");
+// epilogue (halo_epilogue<16>): park 128 rows x 132 fp32, two 32 KB residual pass buffers; pass 0's
+// residual lands in the halo buffer the last channel block does not read (index = ncb & 1)
+constexpr int PK = 128 * (BN + 4) * 4, RB = 128 * BN * 2;
+static_assert(RB <= HBYTES && HBYTES + RB + PK <= LDS && HBYTES + PK + RB <= LDS, "epilogue plan");
+__device__ __forceinline__ int res_off(int f, int p) { return ((p & 1) == 0) ? (f ? HBYTES : 0) : (f ? 0 : HBYTES + PK); }
+__device__ __forceinline__ int park_off(int f) { return f ? HBYTES + RB : HBYTES; }
+__device__ __forceinline__ int sw(int s) { return ((s >> 2) & 1) << 1; }
+}  // namespace halo8
+
+// vmcnt(n) for a wave-uniform runtime n in [0, 7]
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    default: wait_vm<7>(); break;
+  }
+}
+
+template <int GN>
+__global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
+                                                            unsigned bytesw) {
+  using namespace halo8;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const hbuf = lds;
+  char* const bbuf = lds + 2 * HBYTES;
+  float* const abl = reinterpret_cast<float*>(lds + TABLE);
+  const int tn = a.cout / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;  // XCD-aware bijective remap (as conv3x3_halo_kernel)
+  const int xcd = orig & 7, q8 = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (orig >> 3);
+  const int nt = wgid % tn;
+  int sp = wgid / tn;
+  const int tx = sp % tiles_x;
+  sp /= tiles_x;
+  const int ty = sp % tiles_y, img = sp / tiles_y;
+  const int oy0 = ty * TR, ox0 = tx * TC, n0 = nt * BN;
+  const int H = a.h, W = a.w, cin = a.c0;
+  const int ncb = cin >> 5, U = ncb * 9;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;  // wave = (output row, 64-channel half)
+  const bool wload = wave < 8;              // weight-stream wave; else halo-stream wave
+  const int hw = wave - 8;
+
+  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)bytes0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)a.weight, (short)0, (int)bytesw, 0x00020000);
+  const bool res_dma = a.res != nullptr;
+  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(res_dma ? a.res : a.in0), (short)0, res_dma ? (int)((long)(img * H + H) * W * a.res_ld * 2) : 0, 0x00020000);
+  const int f = ncb & 1;  // the halo buffer the last channel block does not read
+
+  // halo waves: pieces hw + 8 k (k < 6; past the 42 pieces, piece hw + 32 again: same bytes, same slots).
+  // A piece's source offset (or out-of-image zeros) is recomputed at each issue from a laundered lane id
+  // (six live offsets would push the 128-VGPR loop into scratch); hinfo keeps, per piece, a valid bit
+  // (real piece, inside the image: transform it) and the lane's logical channel chunk (bits 8 + 2k).
+  auto hpiece = [&](int k) { return hw + 8 * k < NPIECE ? hw + 8 * k : hw + 32; };  // wave-uniform
+  auto halo_voff = [&](int k, int ln) {
+    const int p = hpiece(k);
+    const int sl = p * 16 + (ln >> 2), ph = ln & 3;
+    unsigned vo = kOOB;
+    if (sl < HPIX) {
+      const int hr = sl / HC, hc = sl - (sl / HC) * HC;
+      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        vo = (unsigned)((img * H + iy) * W + ix) * (unsigned)(a.ld0 * 2) + (unsigned)((ph ^ sw(sl)) * 16);
+    }
+    return vo;
+  };
+  unsigned hinfo = 0;
+  if (!wload) {
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) {
+      const int sl = hpiece(k) * 16 + (lane >> 2);
+      if (hw + 8 * k < NPIECE && halo_voff(k, lane) != kOOB) hinfo |= 1u << k;
+      hinfo |= (unsigned)((lane & 3) ^ sw(sl)) << (8 + 2 * k);
+    }
+  }
+  auto hpo = [&](int k) { return hpiece(k) * 1024; };
+  auto issue_halo = [&](int cb) {
+    char* dst = hbuf + (cb & 1) * HBYTES;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) dma16(rs0, dst + hpo(k), halo_voff(k, ln), cb * 64);
+  };
+  // weight waves: rows n = 16 wave + lane / 4, chunk lane % 4 of every tap slice
+  unsigned bvo = kOOB;
+  if (wload) {
+    const int n = wave * 16 + (lane >> 2), ph = lane & 3;
+    bvo = (n0 + n < a.cout) ? (unsigned)(n0 + n) * (unsigned)(a.wld * 2) + (unsigned)((ph ^ sw(n)) * 16) : kOOB;
+  }
+  auto issue_b = [&](int u) {
+    const int cb = u / 9, t = u - (u / 9) * 9;
+    dma16(rsw, bbuf + (u % NB) * BBYTES + wave * 1024, bvo, (t * cin + cb * 32) * 2);
+  };
+  auto transform = [&](int cb) {  // halo waves: their real pieces of block cb, in place
+    char* hb = hbuf + (cb & 1) * HBYTES + lane * 16;
+#pragma unroll 1
+    for (int k = 0; k < PPW; ++k) {  // one piece at a time (register budget)
+      if (!(hinfo & (1u << k))) continue;
+      char* pc = hb + hpo(k);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(pc);
+      const int ch = (hinfo >> (8 + 2 * k)) & 3;
+      const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
+      const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
+      const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+      const float bv[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = __builtin_fmaf((float)v[e], av[e], bv[e]);
+        if constexpr (GN == 2) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+        o[e] = (bf16)x;
+      }
+      *reinterpret_cast<bf16x8*>(pc) = o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: halo waves bring the table (one piece each; waves past its pieces repeat piece 0) and
+  // block 0's halo; weight waves the first LEAD slices
+  if (wload) {
+    const int n0s = U < LEAD ? U : LEAD;
+    for (int u = 0; u < n0s; ++u) issue_b(u);
+  } else {
+    if constexpr (GN != 0) {
+      const int tbytes = cin * 8, tp = hw < (tbytes + 1023) / 1024 ? hw : 0;
+      const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.gn_ab + (long)img * cin * 2), (short)0, tbytes, 0x00020000);
+      dma16(rst, reinterpret_cast<char*>(abl) + tp * 1024, (unsigned)(tp * 1024 + lane * 16), 0);
+    }
+    issue_halo(0);
+    wait_vm<0>();
+  }
+  if constexpr (GN != 0) {
+    __syncthreads();  // every table piece has landed
+    if (!wload) transform(0);
+  }
+
+  const int lr = lane & 15, lq = lane >> 4;
+  const int bsw = (lq ^ sw(lr)) * 16;
+  for (int cb = 0; cb < ncb; ++cb) {
+    const bool more = cb + 1 < ncb;
+    const char* hb = hbuf + (cb & 1) * HBYTES;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int u = cb * 9 + t;
+      if (wload) {  // slice u landed; younger: the slices issued after it (and at the last tap the residual)
+        const int ahead = U - 1 - u < LEAD - 1 ? U - 1 - u : LEAD - 1;
+        wait_vm_rt(ahead + (res_dma && u == U - 1 ? 2 : 0));
+      } else if (t == 8 && !more && res_dma) {
+        wait_vm<2>();  // nothing of the halo stream is outstanding (the residual is younger)
+      }
+      if constexpr (GN != 0)
+        if (t == 2 && more && !wload) {  // own pieces of the next block (issued at tap 0)
+          wait_vm<0>();
+          transform(cb + 1);
+        }
+      __builtin_amdgcn_s_barrier();
+      if (wload) {
+        if (u + LEAD < U) issue_b(u + LEAD);
+      } else if (t == 0 && more) {
+        issue_halo(cb + 1);
+      }
+      if (t == 7 && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
+        halo_res_dma<NW>(rsr, lds + res_off(f, 0), (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
+      const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
+      const int ky = t / 3, kx = t - (t / 3) * 3;
+      bf16x8 bfv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
+      int lb = wm * HC + lr;
+      asm volatile("" : "+v"(lb));
+      const int sl = lb + ky * HC + kx;
+      const char* ab = hb + sl * 64 + ((lq ^ sw(sl)) << 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  halo_epilogue<NW>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(f), res_off(f, 0),
+                    res_off(f, 1), rsr, wave);
+}
+
+int g_halo8 = 1;  // the 8-row halo conv where it applies (rdeic_set_conv_option(9, v))
 
 int g_halo = 1;  // 3x3 halo conv: 0 off, 1 for GroupNorm-input convs (default), 2 for every eligible conv
 
@@ -1664,11 +1903,21 @@ int launch_halo(const rdeic_conv_desc* d, ConvArgs a, hipStream_t s, bool* fused
     e.gn_row0 = i0 * (int)ipix;
     const unsigned b0 = (unsigned)(((e.n * ipix - 1) * d->ld0 + d->c0) * 2);
     const unsigned bw = (unsigned)((long)d->cout * d->wld * 2);
-    const int tx = d->w / TC, ty = d->h / TR;
-    const long tiles = (long)e.n * ty * tx * (d->cout / BN);
     rdeic_count_launch(RDEIC_COUNT_HALO_CONV);
     const bool fe = !e.out_f32 && !e.emb && e.act == 0;
     const int gm = e.gn_ab ? (e.gn_silu ? 2 : 1) : 0;
+    if (g_halo8 && fe && d->h % halo8::TR == 0) {  // the 8-row, one-block-per-CU form
+      const int tx8 = d->w / halo8::TC, ty8 = d->h / halo8::TR;
+      const dim3 g8((unsigned)((long)e.n * ty8 * tx8 * (d->cout / halo8::BN))), b8(halo8::NT);
+      if (gm == 2) hipLaunchKernelGGL((conv3x3_halo8_kernel<2>), g8, b8, halo8::LDS, s, e, tx8, ty8, b0, bw);
+      else if (gm == 1) hipLaunchKernelGGL((conv3x3_halo8_kernel<1>), g8, b8, halo8::LDS, s, e, tx8, ty8, b0, bw);
+      else hipLaunchKernelGGL((conv3x3_halo8_kernel<0>), g8, b8, halo8::LDS, s, e, tx8, ty8, b0, bw);
+      const int rc = launch_status();
+      if (rc != RDEIC_OK) return rc;
+      continue;
+    }
+    const int tx = d->w / TC, ty = d->h / TR;
+    const long tiles = (long)e.n * ty * tx * (d->cout / BN);
     const dim3 g((unsigned)tiles), b(NT);
     if (gm == 2 && fe) hipLaunchKernelGGL((conv3x3_halo_kernel<2, true>), g, b, LDS, s, e, tx, ty, b0, bw);
     else if (gm == 2) hipLaunchKernelGGL((conv3x3_halo_kernel<2, false>), g, b, LDS, s, e, tx, ty, b0, bw);
@@ -1921,5 +2170,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 5) { int prev = g_dma; g_dma = value; return prev; }
   if (key == 6) { int prev = g_halo; g_halo = value; return prev; }
   if (key == 8) { int prev = rdeic_g_attn512; rdeic_g_attn512 = value; return prev; }
+  if (key == 9) { int prev = g_halo8; g_halo8 = value; return prev; }
   return RDEIC_EINVAL;
 }

@@ -118,3 +118,28 @@ def test_halo_conv_zero_padding_is_of_the_normalised_tensor(gpu):
     d = (y_h.float() - y_m.float()).abs()
     assert d[:, 0].max().item() < 2e-2 * max(1.0, y_m.float().abs().max().item())
     assert d[:, :, 0].max().item() < 2e-2 * max(1.0, y_m.float().abs().max().item())
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout,silu", [(2, 16, 128, 128, 128, True), (1, 8, 64, 512, 512, True),
+                                                 (2, 24, 64, 96, 256, False)])
+def test_halo8_bit_identical_to_halo4(gpu, n, h, w, cin, cout, silu):
+    """The 8-row halo conv (one 1024-thread block per CU, rdeic_set_conv_option(9, 1)) uses the 4-row
+    kernel's MFMA order: outputs, residual epilogue and fused statistics are bit-identical."""
+    from rdeic_amd import ops
+    torch.manual_seed(h * cin + cout)
+    x = (torch.randn(n, h, w, cin, device="cuda") * 1.3 - 0.2).to(torch.bfloat16)
+    _, _, p = _params(cin, cout, seed=cin * 7 + cout)
+    ab = _gn_ab(x, 32, seed=11)
+    res = torch.randn(n, h, w, cout, device="cuda").to(torch.bfloat16)
+    outs = []
+    for mode in (1, 0):
+        prev = ops.set_conv_option(9, mode)
+        try:
+            y = _run(x, p, ab, silu=silu, res=res, stats=True)
+            gamma, beta = torch.ones(cout, device="cuda"), torch.zeros(cout, device="cuda")
+            outs.append((y, ops.group_norm_ab(y, gamma, beta, 32, 1e-6)))
+        finally:
+            ops.set_conv_option(9, prev)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -20,3 +20,6 @@ for l in open('gpurun_out/r04f/halo.jsonl'):
 PY
 timeout -k 10 300 python -u -m pytest -q -x --timeout 200 --timeout-method thread tests/test_halo_conv_gpu.py > $O/pytest.log 2>&1 || { echo "halo tests failed"; tail -30 $O/pytest.log; exit 4; }
 tail -2 $O/pytest.log
+timeout -k 10 200 python -u tools/halo_bench.py unet > $O/halo_bench_unet.txt 2>&1 || { echo "halo_bench unet failed"; exit 5; }
+timeout -k 10 200 python -u tools/halo_bench.py > $O/halo_bench_vae.txt 2>&1 || { echo "halo_bench vae failed"; exit 5; }
+cat $O/halo_bench_unet.txt $O/halo_bench_vae.txt

@@ -26,10 +26,17 @@ def timeit(fn, reps=10):
     return e0.elapsed_time(e1) / reps
 
 
+# UNet-ResBlock-like shapes the halo kernel can take (64-pixel rows, cout % 128): the in_layers conv
+# carries the timestep embedding (emb); the UNet's own widths (320 / 640 / 1280 at 64^2..8^2) need a
+# 160-wide N tile and narrower image rows, so these bracket what a fused UNet ResBlock conv would gain
+SHAPES_UNET = [(16, 64, 64, 256, 256), (16, 64, 64, 384, 384), (16, 64, 64, 512, 512)]
+
+
 def main():
     only = sys.argv[1:]
-    for n, h, w, cin, cout in SHAPES:
-        if only and f"{h}x{cin}x{cout}" not in only:
+    unet = "unet" in only
+    for n, h, w, cin, cout in (SHAPES_UNET if unet else SHAPES):
+        if only and not unet and f"{h}x{cin}x{cout}" not in only:
             continue
         x = torch.randn(n, h, w, cin, device="cuda").to(torch.bfloat16)
         wt = torch.randn(cout, cin, 3, 3, device="cuda") / math.sqrt(cin * 9)
@@ -39,13 +46,15 @@ def main():
         res = torch.randn(n, h, w, cout, device="cuda").to(torch.bfloat16)
         out = torch.empty(n, h, w, cout, device="cuda", dtype=torch.bfloat16)
         flops = 2.0 * n * h * w * cout * 9 * cin
+        emb = torch.randn(n, cout, device="cuda") if unet else None
         r = {}
         for mode in (0, 1):
             ops.set_halo_conv(mode)
-            ms = timeit(lambda: ops.conv2d(x, p, gn=ab, gn_silu=True, res=res, out=out, stats=True))
+            ms = timeit(lambda: ops.conv2d(x, p, gn=ab, gn_silu=True, emb=emb, res=None if unet else res, out=out,
+                                           stats=True))
             r[mode] = ms
         ops.set_halo_conv(1)
-        print(f"{n}x{h}x{w} {cin}->{cout}: materialised {r[0]:.3f} ms ({flops / r[0] / 1e9:.0f} TF eff), "
+        print(f"{n}x{h}x{w} {cin}->{cout}{' +emb' if unet else ''}: materialised {r[0]:.3f} ms ({flops / r[0] / 1e9:.0f} TF eff), "
               f"halo {r[1]:.3f} ms ({flops / r[1] / 1e9:.0f} TF)", flush=True)
 
 
