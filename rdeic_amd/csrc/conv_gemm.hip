@@ -1702,6 +1702,13 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
   char* const hbuf = lds;
   char* const bbuf = lds + 2 * HBYTES;
   float* const abl = reinterpret_cast<float*>(lds + TABLE);
+  HALO_STAMP(0);
+#ifdef RDEIC_HALO_STAMPS
+  if (threadIdx.x == 0) {
+    g_halo_stamps[(long)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    g_halo_stamps[(long)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
+#endif
   const int tn = a.cout / BN;
   const int nwg = gridDim.x, orig = blockIdx.x;  // XCD-aware bijective remap (as conv3x3_halo_kernel)
   const int xcd = orig & 7, q8 = nwg >> 3, rr = nwg & 7;
@@ -1821,6 +1828,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     if (!wload) transform(0);
   }
 
+  HALO_STAMP(1);
   const int lr = lane & 15, lq = lane >> 4;
   const int bsw = (lq ^ sw(lr)) * 16;
   for (int cb = 0; cb < ncb; ++cb) {
@@ -1829,18 +1837,20 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int u = cb * 9 + t;
-      if (wload) {  // slice u landed; younger: the slices issued after it (and at the last tap the residual)
+      if (RDEIC_HALO_DIAG & 1) {
+        if (t == 8 && !more) wait_vm<0>();
+      } else if (wload) {  // slice u landed; younger: the slices issued after it (and at the last tap the residual)
         const int ahead = U - 1 - u < LEAD - 1 ? U - 1 - u : LEAD - 1;
         wait_vm_rt(ahead + (res_dma && u == U - 1 ? 2 : 0));
       } else if (t == 8 && !more && res_dma) {
         wait_vm<2>();  // nothing of the halo stream is outstanding (the residual is younger)
       }
-      if constexpr (GN != 0)
+      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
         if (t == 2 && more && !wload) {  // own pieces of the next block (issued at tap 0)
           wait_vm<0>();
           transform(cb + 1);
         }
-      __builtin_amdgcn_s_barrier();
+      if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (wload) {
         if (u + LEAD < U) issue_b(u + LEAD);
       } else if (t == 0 && more) {
@@ -1861,12 +1871,19 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       for (int i = 0; i < 4; ++i) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          if (RDEIC_HALO_DIAG & 4)
+            asm volatile("" ::"v"(af), "v"(bfv[j]));
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
   }
+  HALO_STAMP(2);
   halo_epilogue<NW>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(f), res_off(f, 0),
                     res_off(f, 1), rsr, wave);
+  HALO_STAMP(3);
 }
 
 int g_halo8 = 1;  // the 8-row halo conv where it applies (rdeic_set_conv_option(9, v))

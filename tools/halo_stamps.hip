@@ -65,7 +65,10 @@ int main(int argc, char** argv) {
   fill_bf16_k<<<4096, 256>>>(res, npx * CO, 3, 2.f, 0.f);
   fill_f32_k<<<64, 256>>>(bias, CO, 4, 0.2f, 0.f);
   fill_f32_k<<<64, 256>>>(ab, (long)N * C * 2, 5, 1.f, 0.5f);
-  const long tiles = (long)N * (H / 4) * (W / 64) * (CO / 128);
+  const int h8 = rdeic_set_conv_option(9, 1);  // read the default back (the 8-row form when H % 8 == 0)
+  rdeic_set_conv_option(9, h8);
+  const int trow = (h8 && H % 8 == 0) ? 8 : 4;
+  const long tiles = (long)N * (H / trow) * (W / 64) * (CO / 128);
   unsigned long long* st;
   CK(hipMalloc(&st, tiles * 8 * 8));
   CK(hipMemset(st, 0, tiles * 8 * 8));
@@ -123,14 +126,14 @@ int main(int argc, char** argv) {
   }
   const double cyc_span = (double)(t1 - t0);
   const double clk_ghz = cyc_span / (ms * 1e6);
-  // MFMA-bound floor per block: (9 taps x cin/32) x 16 MFMA x 16 cycles x 2 waves per SIMD
-  const double floor_main = 9.0 * (C / 32) * 16 * 16 * 2;
+  // MFMA-bound floor per block: (9 taps x cin/32) x 16 MFMA x 16 cycles x waves per SIMD (2 or 4)
+  const double floor_main = 9.0 * (C / 32) * 16 * 16 * (trow / 2);
   printf("{\"shape\": [%d, %d, %d, %d, %d], \"res\": %d, \"stats\": %d, \"ms\": %.4f, \"tflops\": %.1f, "
          "\"blocks\": %ld, \"cus_seen\": %zu, \"clock_ghz_est\": %.3f, \"blocks_in_flight_per_cu\": %.2f, "
          "\"cycles\": {\"prologue_med\": %.0f, \"main_med\": %.0f, \"main_p90\": %.0f, \"epilogue_med\": %.0f, "
-         "\"epilogue_p90\": %.0f, \"block_med\": %.0f}, \"main_floor_cycles_2waves_per_simd\": %.0f}\n",
+         "\"epilogue_p90\": %.0f, \"block_med\": %.0f}, \"main_floor_cycles\": %.0f, \"tile_rows\": %d}\n",
          N, H, W, C, CO, use_res, use_stats, ms, flops / (ms * 1e-3) / 1e12, tiles, per_cu.size(), clk_ghz,
          conc / per_cu.size(), pct(pro, .5), pct(mainl, .5), pct(mainl, .9), pct(epi, .5), pct(epi, .9), pct(tot, .5),
-         floor_main);
+         floor_main, trow);
   return 0;
 }
