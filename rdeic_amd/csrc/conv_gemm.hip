@@ -1428,6 +1428,9 @@ __device__ unsigned long long* g_halo_stamps;
 #ifndef RDEIC_HALO_DIAG
 #define RDEIC_HALO_DIAG 0
 #endif
+#ifndef RDEIC_HALO8_SPREAD
+#define RDEIC_HALO8_SPREAD 0  // A/B build switch (tools/halo_stamps.hip): see conv3x3_halo8_kernel
+#endif
 
 // GN: 0 plain conv, 1 GroupNorm affine on the input, 2 affine + SiLU (compile-time: no per-element branch);
 // FE: the fast epilogue (halo_epilogue: bf16 out, no emb / activation), else epilogue_vec
@@ -1778,12 +1781,11 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     const int cb = u / 9, t = u - (u / 9) * 9;
     dma16(rsw, bbuf + (u % NB) * BBYTES + wave * 1024, bvo, (t * cin + cb * 32) * 2);
   };
-  auto transform = [&](int cb) {  // halo waves: their real pieces of block cb, in place
-    char* hb = hbuf + (cb & 1) * HBYTES + lane * 16;
-#pragma unroll 1
-    for (int k = 0; k < PPW; ++k) {  // one piece at a time (register budget)
-      if (!(hinfo & (1u << k))) continue;
-      char* pc = hb + hpo(k);
+  // piece k of a halo wave's pieces of block cb, in place (skipped: duplicates and out-of-image chunks)
+  auto transform_piece = [&](int cb, int k) {
+    if (!(hinfo & (1u << k))) return;
+    char* pc = hbuf + (cb & 1) * HBYTES + lane * 16 + hpo(k);
+    {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(pc);
       const int ch = (hinfo >> (8 + 2 * k)) & 3;
       const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
@@ -1799,6 +1801,10 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       }
       *reinterpret_cast<bf16x8*>(pc) = o;
     }
+  };
+  auto transform = [&](int cb) {  // halo waves: all their real pieces of block cb
+#pragma unroll 1
+    for (int k = 0; k < PPW; ++k) transform_piece(cb, k);  // one piece at a time (register budget)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
   };
 
@@ -1846,9 +1852,9 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
         wait_vm<2>();  // nothing of the halo stream is outstanding (the residual is younger)
       }
       if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
-        if (t == 2 && more && !wload) {  // own pieces of the next block (issued at tap 0)
+        if (t == 2 && more && !wload) {  // own pieces of the next block (issued at tap 0) have landed
           wait_vm<0>();
-          transform(cb + 1);
+          if (!RDEIC_HALO8_SPREAD) transform(cb + 1);
         }
       if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (wload) {
@@ -1878,6 +1884,13 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
         }
       }
+      // RDEIC_HALO8_SPREAD: the next block's transform one piece per tap over taps 2..7, after this tap's
+      // MFMAs in program order (its VALU beside the matrix pipe, not in front of the barrier)
+      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
+        if (RDEIC_HALO8_SPREAD && t >= 2 && t < 2 + PPW && more && !wload) {
+          transform_piece(cb + 1, t - 2);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier
+        }
     }
   }
   HALO_STAMP(2);

@@ -65,7 +65,8 @@ int main(int argc, char** argv) {
   fill_bf16_k<<<4096, 256>>>(res, npx * CO, 3, 2.f, 0.f);
   fill_f32_k<<<64, 256>>>(bias, CO, 4, 0.2f, 0.f);
   fill_f32_k<<<64, 256>>>(ab, (long)N * C * 2, 5, 1.f, 0.5f);
-  const int h8 = rdeic_set_conv_option(9, 1);  // read the default back (the 8-row form when H % 8 == 0)
+  // HALO4=1 in the environment: the 4-row kernel everywhere (option 9 off)
+  const int h8 = getenv("HALO4") && atoi(getenv("HALO4")) ? 0 : 1;
   rdeic_set_conv_option(9, h8);
   const int trow = (h8 && H % 8 == 0) ? 8 : 4;
   const long tiles = (long)N * (H / trow) * (W / 64) * (CO / 128);
