@@ -285,9 +285,16 @@ def main():
                 "kernel_share_of_step": round(ms * 1e-3 / prof["_wall_s"], 4),
                 "single_session_ms_per_step": round(prof["_wall_s"] / args.steps * 1e3, 2)}
         # secondary kernels the north star names: attention on MFMA, GroupNorm on HBM
+        if "conv_bytes" in prof:  # algorithmic bytes of every conv launch (input once, weight, output, residual)
+            nb, byts, _ = prof["conv_bytes"]
+            roof["algorithmic_bytes_per_launch"] = round(byts / max(1, nb))
+            roof["algorithmic_bytes_per_step"] = round(byts / args.steps)
+            tb = roof["traffic"].get("bytes_per_launch") if isinstance(roof["traffic"], dict) else None
+            if tb:
+                roof["traffic_over_algorithmic"] = round(tb / (byts / max(1, nb)), 3)
         sec = {}
         for kind, v in prof.items():
-            if kind == "conv" or kind.startswith("_"):
+            if kind in ("conv", "conv_bytes") or kind.startswith("_"):
                 continue
             cnt, work, kms = v
             if kms <= 0:

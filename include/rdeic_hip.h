@@ -326,6 +326,8 @@ int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row);
 #define RDEIC_PROF_GN_APPLY 4    /* rdeic_groupnorm_apply: bytes read + written */
 #define RDEIC_PROF_GEMM 5        /* rdeic_gemm_strided (training backward / attention): 2*M*N*K*batch FLOPs */
 #define RDEIC_PROF_ATTN_D512 6   /* rdeic_attention, head dim 512 (VAE AttnBlock flash kernel): 4*B*Lq*Lk*512 FLOPs */
+#define RDEIC_PROF_CONV_BYTES 7  /* every conv launch (not sampled, no events): algorithmic HBM bytes — input
+                                    (each element once), packed weight, output, residual — ms reads 0 */
 int rdeic_prof_start(int32_t capacity, int32_t every);
 /* Launch counters (always on, one relaxed atomic add per launch): which kernel a dispatcher chose,
  * so tests can assert that a fused path actually ran (e.g. the halo conv, not its fallback). */

@@ -2088,6 +2088,19 @@ static double conv_flops(const rdeic_conv_desc* d) {
   return 2.0 * b * d->n * d->ho * d->wo * d->cout * (double)d->kh * d->kw * (d->c0 + d->c1);
 }
 
+// algorithmic HBM bytes of one launch: every input element once (an upsampled input at its stored size),
+// the packed weight once, the output, the residual (RDEIC_PROF_CONV_BYTES)
+static double conv_bytes(const rdeic_conv_desc* d) {
+  if (!d) return 0.0;
+  const double b = d->batch > 1 ? d->batch : 1;
+  const double es = d->dtype == 1 ? 2.0 : 4.0, os = (d->dtype == 0 || d->out_f32) ? 4.0 : 2.0;
+  const double in = b * d->n * (double)d->h * d->w * (d->c0 + d->c1) * es;
+  const double w = (double)(d->batch > 1 ? b : 1) * d->cout * d->wld * es;
+  double outc = d->out_mode == 2 ? d->cout / 2.0 : (double)d->cout;
+  const double out = b * d->n * (d->out_mode == 1 ? 4.0 : 1.0) * d->ho * d->wo * (d->out_mode == 1 ? outc / 4 : outc) * os;
+  return in + w + out + (d->res ? out : 0.0);
+}
+
 // d->gn_part: the output's GroupNorm statistics in the partial format of rdeic_groupnorm_parts_ab,
 // fused into the epilogue where the launch allows it, else by a separate pass over the output.
 static int conv2d_impl(const rdeic_conv_desc* d, int32_t tile, void* stream) {
@@ -2097,6 +2110,7 @@ static int conv2d_impl(const rdeic_conv_desc* d, int32_t tile, void* stream) {
   bool fused = false;
   int rc;
   {
+    rdeic_prof_add_bytes(conv_bytes(d));
     ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
     rc = tile == -2 ? conv2d_run(d, stream, &fused) : conv2d_tile_run(d, tile, stream, &fused);
   }
@@ -2174,6 +2188,7 @@ extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, flo
     return RDEIC_EINVAL;
   int rc;
   {
+    rdeic_prof_add_bytes(conv_bytes(d));
     ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
     rc = conv2d_splitk_impl(d, splits, ws, ws_floats, stream);
   }

@@ -7,6 +7,7 @@
 
 void rdeic_count_launch(int kind);  // RDEIC_COUNT_* (include/rdeic_hip.h): which kernel family a launcher chose
 
+void rdeic_prof_add_bytes(double bytes);  // RDEIC_PROF_CONV_BYTES accumulator (no-op when profiling is off)
 int rdeic_prof_begin(hipStream_t s, int kind, double work);           // slot, or -1 (off / full / not sampled)
 void rdeic_prof_end(int slot, hipStream_t s, int kind, double work);  // no-op for slot < 0
 

@@ -36,6 +36,7 @@ int g_used = 0;
 bool g_on = false;
 int g_every = 1;     // time one small launch in g_every (per kind)
 long g_seen[8] = {};
+double g_bytes_n = 0.0, g_bytes = 0.0;  // RDEIC_PROF_CONV_BYTES (every launch while profiling)
 std::mutex g_mu;
 
 double always_threshold(int kind) {
@@ -66,6 +67,14 @@ int rdeic_prof_begin(hipStream_t s, int kind, double work) {
   return i;
 }
 
+void rdeic_prof_add_bytes(double bytes) {
+  if (!g_on) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_on) return;
+  g_bytes_n += 1.0;
+  g_bytes += bytes;
+}
+
 void rdeic_prof_end(int slot, hipStream_t s, int kind, double work) {
   if (slot < 0) return;
   std::lock_guard<std::mutex> lk(g_mu);
@@ -88,6 +97,7 @@ extern "C" int rdeic_prof_start(int32_t capacity, int32_t every) {
     g_slots.push_back(sl);
   }
   g_used = 0;
+  g_bytes_n = g_bytes = 0.0;
   g_every = every;
   for (long& c : g_seen) c = 0;
   g_on = true;
@@ -103,6 +113,10 @@ extern "C" int rdeic_prof_stop(void) {
 extern "C" int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, double* ms) {
   if (!launches || !work || !ms) return RDEIC_EINVAL;
   std::lock_guard<std::mutex> lk(g_mu);
+  if (kind == RDEIC_PROF_CONV_BYTES) {
+    *launches = (int64_t)(g_bytes_n + 0.5); *work = g_bytes; *ms = 0.0;
+    return RDEIC_OK;
+  }
   double n = 0.0, w = 0.0, t_ms = 0.0;
   for (int i = 0; i < g_used; ++i) {
     const Slot& sl = g_slots[i];

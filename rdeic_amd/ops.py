@@ -420,7 +420,7 @@ def record_profile(tag, ev0, ev1):
 
 
 PROF_KINDS = {"conv": 0, "attention": 1, "attention_dh16": 2, "gn_stats": 3, "gn_apply": 4, "gemm": 5,
-              "attention_d512": 6}
+              "attention_d512": 6, "conv_bytes": 7}
 
 
 def prof_start(capacity: int = 65536, every: int = 1) -> None:
