@@ -1764,6 +1764,11 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     }
   }
   auto hpo = [&](int k) { return hpiece(k) * 1024; };
+  auto issue_halo_piece = [&](int cb, int k) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    dma16(rs0, hbuf + (cb & 1) * HBYTES + hpo(k), halo_voff(k, ln), cb * 64);
+  };
   auto issue_halo = [&](int cb) {
     char* dst = hbuf + (cb & 1) * HBYTES;
     int ln = lane;
@@ -1851,14 +1856,22 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       } else if (t == 8 && !more && res_dma) {
         wait_vm<2>();  // nothing of the halo stream is outstanding (the residual is younger)
       }
-      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
-        if (t == 2 && more && !wload) {  // own pieces of the next block (issued at tap 0) have landed
+      if (!wload && more && !(RDEIC_HALO_DIAG & 1)) {  // this wave's pieces of the next block have landed
+        if (RDEIC_HALO8_SPREAD >= 2) {
+          if (t >= 2 && t < 2 + PPW) {  // piece t - 2 (issued two taps ago); younger: piece t - 1 if issued
+            if (t - 1 < PPW) wait_vm<1>(); else wait_vm<0>();
+          }
+        } else if (t == 2) {  // all six (issued at tap 0)
           wait_vm<0>();
-          if (!RDEIC_HALO8_SPREAD) transform(cb + 1);
         }
+      }
+      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
+        if (RDEIC_HALO8_SPREAD == 0 && t == 2 && more && !wload) transform(cb + 1);
       if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (wload) {
         if (u + LEAD < U) issue_b(u + LEAD);
+      } else if (RDEIC_HALO8_SPREAD >= 2) {
+        if (t < PPW && more) issue_halo_piece(cb + 1, t);  // piece t, transformed at tap t + 2
       } else if (t == 0 && more) {
         issue_halo(cb + 1);
       }
