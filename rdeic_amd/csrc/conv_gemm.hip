@@ -1755,7 +1755,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     return vo;
   };
   unsigned hinfo = 0;
-  if (!wload) {
+  if (!wload && RDEIC_HALO8_SPREAD != 3) {
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
       const int sl = hpiece(k) * 16 + (lane >> 2);
@@ -1764,6 +1764,24 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     }
   }
   auto hpo = [&](int k) { return hpiece(k) * 1024; };
+  // RDEIC_HALO8_SPREAD == 3: the transform is balanced over all 16 waves, wave w taking pieces
+  // w + 16 k (k < 3, < 42) whoever loaded them; tinfo: per k a valid bit (bit k) and the chunk (bits 8 + 2k)
+  unsigned tinfo = 0;
+  if (RDEIC_HALO8_SPREAD == 3) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int p = wave + 16 * k;
+      const int sl = p * 16 + (lane >> 2), ph = lane & 3;
+      bool in = false;
+      if (p < NPIECE && sl < HPIX) {
+        const int hr = sl / HC, hc = sl - (sl / HC) * HC;
+        const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+        in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      }
+      if (in) tinfo |= 1u << k;
+      tinfo |= (unsigned)(ph ^ sw(sl)) << (8 + 2 * k);
+    }
+  }
   auto issue_halo_piece = [&](int cb, int k) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
@@ -1786,13 +1804,15 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     const int cb = u / 9, t = u - (u / 9) * 9;
     dma16(rsw, bbuf + (u % NB) * BBYTES + wave * 1024, bvo, (t * cin + cb * 32) * 2);
   };
-  // piece k of a halo wave's pieces of block cb, in place (skipped: duplicates and out-of-image chunks)
+  // piece k of a halo wave's pieces of block cb, in place (skipped: duplicates and out-of-image chunks);
+  // SPREAD == 3: piece wave + 16 k of the block, whoever loaded it
   auto transform_piece = [&](int cb, int k) {
-    if (!(hinfo & (1u << k))) return;
-    char* pc = hbuf + (cb & 1) * HBYTES + lane * 16 + hpo(k);
+    const unsigned info = RDEIC_HALO8_SPREAD == 3 ? tinfo : hinfo;
+    if (!(info & (1u << k))) return;
+    char* pc = hbuf + (cb & 1) * HBYTES + lane * 16 + (RDEIC_HALO8_SPREAD == 3 ? (wave + 16 * k) * 1024 : hpo(k));
     {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(pc);
-      const int ch = (hinfo >> (8 + 2 * k)) & 3;
+      const int ch = (info >> (8 + 2 * k)) & 3;
       const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
       const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
       const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
@@ -1857,7 +1877,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
         wait_vm<2>();  // nothing of the halo stream is outstanding (the residual is younger)
       }
       if (!wload && more && !(RDEIC_HALO_DIAG & 1)) {  // this wave's pieces of the next block have landed
-        if (RDEIC_HALO8_SPREAD >= 2) {
+        if (RDEIC_HALO8_SPREAD == 2) {
           if (t >= 2 && t < 2 + PPW) {  // piece t - 2 (issued two taps ago); younger: piece t - 1 if issued
             if (t - 1 < PPW) wait_vm<1>(); else wait_vm<0>();
           }
@@ -1870,7 +1890,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
       if (wload) {
         if (u + LEAD < U) issue_b(u + LEAD);
-      } else if (RDEIC_HALO8_SPREAD >= 2) {
+      } else if (RDEIC_HALO8_SPREAD == 2) {
         if (t < PPW && more) issue_halo_piece(cb + 1, t);  // piece t, transformed at tap t + 2
       } else if (t == 0 && more) {
         issue_halo(cb + 1);
@@ -1897,13 +1917,20 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
         }
       }
-      // RDEIC_HALO8_SPREAD: the next block's transform one piece per tap over taps 2..7, after this tap's
-      // MFMAs in program order (its VALU beside the matrix pipe, not in front of the barrier)
-      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
-        if (RDEIC_HALO8_SPREAD && t >= 2 && t < 2 + PPW && more && !wload) {
+      // RDEIC_HALO8_SPREAD 1 / 2: the next block's transform one piece per tap over taps 2..7 by its loader,
+      // after this tap's MFMAs in program order (its VALU beside the matrix pipe, not in front of the
+      // barrier); 3: pieces wave + 16 k, k = 0..2, by every wave at taps 2..4 (the loaders' tap-2 wait and
+      // barrier made them visible)
+      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8)) {
+        if ((RDEIC_HALO8_SPREAD == 1 || RDEIC_HALO8_SPREAD == 2) && t >= 2 && t < 2 + PPW && more && !wload) {
           transform_piece(cb + 1, t - 2);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier
         }
+        if (RDEIC_HALO8_SPREAD == 3 && t >= 2 && t < 5 && more) {
+          transform_piece(cb + 1, t - 2);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+      }
     }
   }
   HALO_STAMP(2);
