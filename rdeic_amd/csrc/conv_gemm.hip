@@ -1431,6 +1431,9 @@ __device__ unsigned long long* g_halo_stamps;
 #ifndef RDEIC_HALO8_SPREAD
 #define RDEIC_HALO8_SPREAD 0  // A/B build switch (tools/halo_stamps.hip): see conv3x3_halo8_kernel
 #endif
+#ifndef RDEIC_HALO8_BAR2
+#define RDEIC_HALO8_BAR2 0  // A/B build switch: one barrier per two taps in conv3x3_halo8_kernel
+#endif
 
 // GN: 0 plain conv, 1 GroupNorm affine on the input, 2 affine + SiLU (compile-time: no per-element branch);
 // FE: the fast epilogue (halo_epilogue: bf16 out, no emb / activation), else epilogue_vec
@@ -1868,8 +1871,17 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int u = cb * 9 + t;
+      // BAR2: barriers (and every wait and DMA issue) only at even taps of a channel block; the odd tap
+      // after one reads the slice the same barrier published
+      const bool BAR = !RDEIC_HALO8_BAR2 || (t % 2 == 0);  // t is unrolled: a compile-time value
       if (RDEIC_HALO_DIAG & 1) {
         if (t == 8 && !more) wait_vm<0>();
+      } else if (RDEIC_HALO8_BAR2) {
+        if (wload && BAR) {  // slices u and (t < 8) u + 1 landed; issued so far: up to u + 5
+          const int issued = u + 5 < U - 1 ? u + 5 : U - 1;
+          const int need = (t < 8 && u + 1 < U) ? u + 1 : u;
+          wait_vm_rt(issued - need);
+        }
       } else if (wload) {  // slice u landed; younger: the slices issued after it (and at the last tap the residual)
         const int ahead = U - 1 - u < LEAD - 1 ? U - 1 - u : LEAD - 1;
         wait_vm_rt(ahead + (res_dma && u == U - 1 ? 2 : 0));
@@ -1887,15 +1899,22 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       }
       if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
         if (RDEIC_HALO8_SPREAD == 0 && t == 2 && more && !wload) transform(cb + 1);
-      if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
+      if (!(RDEIC_HALO_DIAG & 2) && BAR) __builtin_amdgcn_s_barrier();
       if (wload) {
-        if (u + LEAD < U) issue_b(u + LEAD);
+        if (RDEIC_HALO8_BAR2) {
+          if (BAR) {  // slices u + 6 and (t < 8) u + 7: slots last read at taps u - 2 and u - 1
+            if (u + LEAD < U) issue_b(u + LEAD);
+            if (t < 8 && u + LEAD + 1 < U) issue_b(u + LEAD + 1);
+          }
+        } else if (u + LEAD < U) {
+          issue_b(u + LEAD);
+        }
       } else if (RDEIC_HALO8_SPREAD == 2) {
         if (t < PPW && more) issue_halo_piece(cb + 1, t);  // piece t, transformed at tap t + 2
       } else if (t == 0 && more) {
         issue_halo(cb + 1);
       }
-      if (t == 7 && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
+      if (t == (RDEIC_HALO8_BAR2 ? 8 : 7) && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
         halo_res_dma<NW>(rsr, lds + res_off(f, 0), (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
       const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
       const int ky = t / 3, kx = t - (t / 3) * 3;
