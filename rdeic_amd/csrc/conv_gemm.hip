@@ -1858,8 +1858,8 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     wait_vm<0>();
   }
   if constexpr (GN != 0) {
-    __syncthreads();  // every table piece has landed
-    if (!wload) transform(0);
+    __syncthreads();  // every table piece (and, for SPREAD == 3, every halo piece) has landed
+    if (!wload || RDEIC_HALO8_SPREAD == 3) transform(0);
   }
 
   HALO_STAMP(1);

@@ -3,8 +3,10 @@
 set -o pipefail
 O=gpurun_out/r04l
 mkdir -p $O
-RDEIC_LIB=$PWD/rdeic_amd/lib_b2/librdeic_hip.so timeout -k 10 300 python -u -m pytest -q -x --timeout 200 --timeout-method thread tests/test_halo_conv_gpu.py > $O/pytest_b2.log 2>&1 || { echo "halo tests (b2) failed"; tail -40 $O/pytest_b2.log; exit 4; }
-tail -1 $O/pytest_b2.log
+for v in sp3 b2; do
+  RDEIC_LIB=$PWD/rdeic_amd/lib_$v/librdeic_hip.so timeout -k 10 300 python -u -m pytest -q -x --timeout 200 --timeout-method thread tests/test_halo_conv_gpu.py > $O/pytest_$v.log 2>&1 || { echo "halo tests ($v) failed"; tail -30 $O/pytest_$v.log; exit 4; }
+  echo "$v: $(tail -1 $O/pytest_$v.log)"
+done
 run() {  # name binary env
   for cfg in "16 512 512 128 128 1 1" "16 256 256 256 256 1 1" "16 128 128 512 512 1 1" "16 64 64 512 512 1 1" "16 512 512 256 128 1 1"; do
     echo -n "{\"v\": \"$1\", \"r\": " >> $O/halo.jsonl
