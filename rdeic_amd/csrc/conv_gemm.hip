@@ -1429,10 +1429,10 @@ __device__ unsigned long long* g_halo_stamps;
 #define RDEIC_HALO_DIAG 0
 #endif
 #ifndef RDEIC_HALO8_SPREAD
-#define RDEIC_HALO8_SPREAD 0  // A/B build switch (tools/halo_stamps.hip): see conv3x3_halo8_kernel
+#define RDEIC_HALO8_SPREAD 3  // A/B build switch (tools/halo_stamps.hip): see conv3x3_halo8_kernel; 3 measured best (r04)
 #endif
 #ifndef RDEIC_HALO8_BAR2
-#define RDEIC_HALO8_BAR2 0  // A/B build switch: one barrier per two taps in conv3x3_halo8_kernel
+#define RDEIC_HALO8_BAR2 1  // A/B build switch: one barrier per two taps in conv3x3_halo8_kernel (default, r04)
 #endif
 
 // GN: 0 plain conv, 1 GroupNorm affine on the input, 2 affine + SiLU (compile-time: no per-element branch);
