@@ -1431,6 +1431,12 @@ __device__ unsigned long long* g_halo_stamps;
 #ifndef RDEIC_HALO8_SPREAD
 #define RDEIC_HALO8_SPREAD 3  // A/B build switch (tools/halo_stamps.hip): see conv3x3_halo8_kernel; 3 measured best (r04)
 #endif
+#ifndef RDEIC_HALO8_VMFAST
+#define RDEIC_HALO8_VMFAST 1  // A/B build switch: compile-time vmcnt in the weight waves' steady state
+#endif
+#ifndef RDEIC_HALO8_TW
+#define RDEIC_HALO8_TW 4  // A/B build switch: the tap at which the next halo is waited for (transform: taps TW..TW+2); 4 measured best (r04o)
+#endif
 #ifndef RDEIC_HALO8_BAR2
 #define RDEIC_HALO8_BAR2 1  // A/B build switch: one barrier per two taps in conv3x3_halo8_kernel (default, r04)
 #endif
@@ -1880,7 +1886,10 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
         if (wload && BAR) {  // slices u and (t < 8) u + 1 landed; issued so far: up to u + 5
           const int issued = u + 5 < U - 1 ? u + 5 : U - 1;
           const int need = (t < 8 && u + 1 < U) ? u + 1 : u;
-          wait_vm_rt(issued - need);
+          if (RDEIC_HALO8_VMFAST && u + 6 < U)
+            t < 8 ? wait_vm<4>() : wait_vm<5>();  // steady state: a compile-time count (t is unrolled), no branch chain
+          else
+            wait_vm_rt(issued - need);
         }
       } else if (wload) {  // slice u landed; younger: the slices issued after it (and at the last tap the residual)
         const int ahead = U - 1 - u < LEAD - 1 ? U - 1 - u : LEAD - 1;
@@ -1893,14 +1902,15 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
           if (t >= 2 && t < 2 + PPW) {  // piece t - 2 (issued two taps ago); younger: piece t - 1 if issued
             if (t - 1 < PPW) wait_vm<1>(); else wait_vm<0>();
           }
-        } else if (t == 2) {  // all six (issued at tap 0)
+        } else if (t == RDEIC_HALO8_TW) {  // all six (issued at tap 0)
           wait_vm<0>();
         }
       }
       if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
         if (RDEIC_HALO8_SPREAD == 0 && t == 2 && more && !wload) transform(cb + 1);
       if (!(RDEIC_HALO_DIAG & 2) && BAR) __builtin_amdgcn_s_barrier();
-      if (wload) {
+      if (RDEIC_HALO_DIAG & 32) {  // diag: no DMA issued in the main loop
+      } else if (wload) {
         if (RDEIC_HALO8_BAR2) {
           if (BAR) {  // slices u + 6 and (t < 8) u + 7: slots last read at taps u - 2 and u - 1
             if (u + LEAD < U) issue_b(u + LEAD);
@@ -1919,15 +1929,21 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
       const int ky = t / 3, kx = t - (t / 3) * 3;
       bf16x8 bfv[4];
+      using i32x4d = int __attribute__((ext_vector_type(4)));
+      int zq = lane;  // diag 16: fragments from registers, no LDS reads
+      if (RDEIC_HALO_DIAG & 16) asm volatile("" : "+v"(zq));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
+      for (int j = 0; j < 4; ++j)
+        bfv[j] = (RDEIC_HALO_DIAG & 16) ? __builtin_bit_cast(bf16x8, (i32x4d{zq, zq + j, zq ^ j, zq + 7}))
+                                        : *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
       int lb = wm * HC + lr;
       asm volatile("" : "+v"(lb));
       const int sl = lb + ky * HC + kx;
       const char* ab = hb + sl * 64 + ((lq ^ sw(sl)) << 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
+        const bf16x8 af = (RDEIC_HALO_DIAG & 16) ? __builtin_bit_cast(bf16x8, (i32x4d{zq + i, zq, zq - i, zq}))
+                                                 : *reinterpret_cast<const bf16x8*>(ab + i * 1024);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (RDEIC_HALO_DIAG & 4)
@@ -1945,8 +1961,8 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
           transform_piece(cb + 1, t - 2);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier
         }
-        if (RDEIC_HALO8_SPREAD == 3 && t >= 2 && t < 5 && more) {
-          transform_piece(cb + 1, t - 2);
+        if (RDEIC_HALO8_SPREAD == 3 && t >= RDEIC_HALO8_TW && t < RDEIC_HALO8_TW + 3 && more) {
+          transform_piece(cb + 1, t - RDEIC_HALO8_TW);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
       }
