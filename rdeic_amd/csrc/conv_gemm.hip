@@ -1149,6 +1149,8 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
 //   35 512x128/16 S2 (64x64 per wave at cout = 128: the whole 160 KB of LDS, one block per CU),
 //   36 64x128/8 S2 (32x32 per wave: twice the waves of tile 30 on grids of ~256 tiles),
 //   37 128x160/4 S2 and 38 64x160/4 S2 (N = 320 layers: two N tiles, no padded columns)
+// (r04: 16-wave S3 / S4 rings for the short-K linears, 256x128 S3, 128x256 S3, 128x128 S4, were
+//  slower than these S2 tiles on every transformer linear: profiles/r04_linear_tiles.jsonl)
 // Measured (tools/dma_bench.py, one MI355X): 32 is best where a 256x256 grid fills the chip
 // without padding waste (1.19-1.27 PF on the VAE 512-channel layers), 25 on the rest with >= 256
 // 128x128 tiles, the 4-wave 64x128 tile when even that grid cannot fill the chip; 34 often wins
@@ -1433,6 +1435,12 @@ __device__ unsigned long long* g_halo_stamps;
 #endif
 #ifndef RDEIC_HALO8_VMFAST
 #define RDEIC_HALO8_VMFAST 1  // A/B build switch: compile-time vmcnt in the weight waves' steady state
+#endif
+#ifndef RDEIC_HALO8_PRIO
+#define RDEIC_HALO8_PRIO 0  // A/B build switch: s_setprio(1) around each tap's MFMA cluster
+#endif
+#ifndef RDEIC_HALO8_HSPLIT
+#define RDEIC_HALO8_HSPLIT 1  // A/B build switch: the next halo issued in two halves (taps 0 and 2); measured -0.3..0.9% cycles (r04q)
 #endif
 #ifndef RDEIC_HALO8_TW
 #define RDEIC_HALO8_TW 4  // A/B build switch: the tap at which the next halo is waited for (transform: taps TW..TW+2); 4 measured best (r04o)
@@ -1921,6 +1929,14 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
         }
       } else if (RDEIC_HALO8_SPREAD == 2) {
         if (t < PPW && more) issue_halo_piece(cb + 1, t);  // piece t, transformed at tap t + 2
+      } else if (RDEIC_HALO8_HSPLIT && RDEIC_HALO8_TW >= 4 && (t == 0 || t == 2) && more) {
+        // the next halo's six pieces in two halves (taps 0 and 2), so no barrier waits on a wave issuing six
+        char* dst = hbuf + ((cb + 1) & 1) * HBYTES;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int k = (t == 0 ? 0 : PPW / 2); k < (t == 0 ? PPW / 2 : PPW); ++k)
+          dma16(rs0, dst + hpo(k), halo_voff(k, ln), (cb + 1) * 64);
       } else if (t == 0 && more) {
         issue_halo(cb + 1);
       }
@@ -1940,6 +1956,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       asm volatile("" : "+v"(lb));
       const int sl = lb + ky * HC + kx;
       const char* ab = hb + sl * 64 + ((lq ^ sw(sl)) << 4);
+      if (RDEIC_HALO8_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bf16x8 af = (RDEIC_HALO_DIAG & 16) ? __builtin_bit_cast(bf16x8, (i32x4d{zq + i, zq, zq - i, zq}))
@@ -1952,6 +1969,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
         }
       }
+      if (RDEIC_HALO8_PRIO) __builtin_amdgcn_s_setprio(0);
       // RDEIC_HALO8_SPREAD 1 / 2: the next block's transform one piece per tap over taps 2..7 by its loader,
       // after this tap's MFMAs in program order (its VALU beside the matrix pipe, not in front of the
       // barrier); 3: pieces wave + 16 k, k = 0..2, by every wave at taps 2..4 (the loaders' tap-2 wait and

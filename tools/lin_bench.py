@@ -18,7 +18,7 @@ SHAPES = [("qk320@64", 65536, 320, 320, True, False), ("qkv320@64", 65536, 320, 
           ("o640@32", 16384, 640, 640, True, False), ("geglu640@32", 16384, 640, 5120, False, True),
           ("ff2560->640@32", 16384, 2560, 640, True, False), ("o1280@16", 4096, 1280, 1280, True, False),
           ("geglu1280@16", 4096, 1280, 10240, False, True)]
-TILES = (-1, 24, 25, 26, 30, 31, 34, 36, 33, 28)
+TILES = (-1, 21, 22, 24, 25, 26, 27, 30, 31, 32, 33, 34, 36, 37, 38)
 
 
 def main():
