@@ -2,7 +2,7 @@
 (reference inference_partition.py:139-318 process(), :320-352 arguments, :355-571 main()).
 
     python inference_partition.py --input DIR --output DIR [--batch_size 8] [--micro_batch_size 4]
-        [--steps 2] [--sampler ddpm|ddim] [--fp16] [--enable_resize_guard --max_long_side 1024
+        [--steps 2] [--sampler ddpm|ddim] [--bf16 | --fp16] [--enable_resize_guard --max_long_side 1024
         --upsample_to_original] [--save_intermediates] [--max_images N]
 
 What it keeps from the reference:
@@ -21,8 +21,9 @@ What it keeps from the reference:
 What differs, all forced by the offline image or by design:
   * captioning (--use_captions, Qwen2-VL) and OpenCLIP text encoding are out of scope: the seeded
     synthetic context stands in for the "" embedding, and --use_captions is refused;
-  * --fp16 selects the bf16 compute path (the reference's autocast float16 analogue); the default
-    is the fp32 parity path;
+  * --bf16 selects the bf16 compute path; the default is the fp32 parity path. The reference's
+    --fp16 (autocast float16) is accepted and selects the same bf16 path with a notice on stderr:
+    no float16 kernels are built for MI355X;
   * LPIPS needs an AlexNet backbone that is not available offline: the column is NaN; PSNR, SSIM
     and MS-SSIM are computed on the device (rdeic_amd/metrics.py);
   * noise comes from a CPU generator seeded per image (--seed + the image's index in sorted
@@ -176,7 +177,10 @@ def parse_args(argv=None) -> Namespace:
     p.add_argument("--use_captions", action="store_true", help="(refused: Qwen2-VL captioning needs weights)")
     p.add_argument("--batch_size", type=int, default=1, help="images processed together (grouped by resolution)")
     p.add_argument("--micro_batch_size", type=int, default=0, help="chunks of the sampling / decoding stage")
-    p.add_argument("--fp16", action="store_true", help="bf16 compute path (default: fp32 parity path)")
+    p.add_argument("--bf16", action="store_true", help="bf16 compute path (default: fp32 parity path)")
+    p.add_argument("--fp16", action="store_true",
+                   help="the reference's reduced-precision switch (autocast float16); here it selects the bf16 "
+                        "path, with a notice: no float16 kernels are built for MI355X")
     p.add_argument("--profile_memory", action="store_true")
     p.add_argument("--save_intermediates", action="store_true")
     p.add_argument("--latent_format", type=str, default="pt", choices=["pt", "npy"])
@@ -185,7 +189,12 @@ def parse_args(argv=None) -> Namespace:
     p.add_argument("--upsample_to_original", action="store_true")
     p.add_argument("--upsample_method", type=str, default="lanczos", choices=list(RESAMPLE))
     p.add_argument("--suppress_warnings", action="store_true")
-    return p.parse_args(argv)
+    args = p.parse_args(argv)
+    if args.fp16:
+        print("[inference_partition] --fp16: the reduced-precision path computes in bf16 on MI355X "
+              "(float16 autocast is not provided); same as --bf16", file=sys.stderr)
+        args.bf16 = True
+    return args
 
 
 def _load(args):
@@ -196,11 +205,11 @@ def _load(args):
                 part = torch.load(path, map_location="cpu", weights_only=True)
                 sd.update(part.get("state_dict", part))
         from rdeic_amd.rdeic import RDEIC
-        model = RDEIC(compute_dtype=torch.bfloat16 if args.fp16 else torch.float32)
+        model = RDEIC(compute_dtype=torch.bfloat16 if args.bf16 else torch.float32)
         model.load_state_dict(sd, strict=False)
         model.preprocess_model.update(force=True)
         return model
-    return load_model("", "bf16" if args.fp16 else "fp32")
+    return load_model("", "bf16" if args.bf16 else "fp32")
 
 
 def main(argv=None) -> List[Dict]:
