@@ -1436,6 +1436,9 @@ __device__ unsigned long long* g_halo_stamps;
 #ifndef RDEIC_HALO8_VMFAST
 #define RDEIC_HALO8_VMFAST 1  // A/B build switch: compile-time vmcnt in the weight waves' steady state
 #endif
+#ifndef RDEIC_HALO8_LAUNDER
+#define RDEIC_HALO8_LAUNDER 1  // A/B build switch: recompute the transform's offsets in the loop (no scratch)
+#endif
 #ifndef RDEIC_HALO8_PRIO
 #define RDEIC_HALO8_PRIO 0  // A/B build switch: s_setprio(1) around each tap's MFMA cluster
 #endif
@@ -1824,9 +1827,14 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
   // piece k of a halo wave's pieces of block cb, in place (skipped: duplicates and out-of-image chunks);
   // SPREAD == 3: piece wave + 16 k of the block, whoever loaded it
   auto transform_piece = [&](int cb, int k) {
-    const unsigned info = RDEIC_HALO8_SPREAD == 3 ? tinfo : hinfo;
+    // info and lane laundered: their derived offsets are recomputed here instead of hoisted out of the
+    // channel-block loop, where hipcc kept them in scratch; every reload was an s_waitcnt vmcnt(0)
+    // that drained the weight ring's in-flight LDS-DMA (r04)
+    unsigned info = RDEIC_HALO8_SPREAD == 3 ? tinfo : hinfo;
+    int ln = lane;
+    if (RDEIC_HALO8_LAUNDER) asm volatile("" : "+v"(info), "+v"(ln));
     if (!(info & (1u << k))) return;
-    char* pc = hbuf + (cb & 1) * HBYTES + lane * 16 + (RDEIC_HALO8_SPREAD == 3 ? (wave + 16 * k) * 1024 : hpo(k));
+    char* pc = hbuf + (cb & 1) * HBYTES + ln * 16 + (RDEIC_HALO8_SPREAD == 3 ? (wave + 16 * k) * 1024 : hpo(k));
     {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(pc);
       const int ch = (info >> (8 + 2 * k)) & 3;
