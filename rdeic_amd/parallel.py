@@ -24,7 +24,20 @@ def init_from_env(backend: str = None) -> Tuple[int, int, int]:
             backend = os.environ.get("RDEIC_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+            dist.init_process_group(backend=backend)
+        else:
+            # gloo's C++ side prints "[Gloo] Rank i is connected ..." on the process's stdout, which must
+            # carry nothing but rank 0's JSON line: route fd 1 to stderr while the mesh connects
+            import sys
+            sys.stdout.flush()
+            saved = os.dup(1)
+            try:
+                os.dup2(2, 1)
+                dist.init_process_group(backend=backend)
+                dist.barrier()
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return rank, world, local
