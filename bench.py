@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--sampler", default="ddim", choices=["ddim", "ddpm"],
                     help="relay sampler (config 2 names 2-step relay DDIM; ddpm = the CLI's spaced sampler)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=5,
                     help="codec sessions in flight per GPU (host thread + HIP stream each; RDEIC.session): one "
                          "batch's host rANS coding and small entropy-stage kernels overlap another batch's GPU work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
