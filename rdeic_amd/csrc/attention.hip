@@ -209,7 +209,10 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
   // NQ groups of 16 queries per wave share every staged K/V tile of KTL keys (fewer barriers and
   // LDS fills per score); the 2-stage barrier pattern is the generic kernel's.
   static_assert(DH == 16 || DH == 32, "small-head kernel");
-  constexpr int DP = 32;         // QK^T contraction padded to the bf16 MFMA k
+  // QK^T contraction: d = 16 on the k = 16 MFMA (v_mfma_f32_16x16x16_bf16, half the k = 32 form's
+  // cycles and no zero padding), d = 32 on the k = 32 one
+  constexpr bool K16 = DH == 16;
+  constexpr int DP = K16 ? 16 : 32;
   constexpr int KROW = DP + 8;   // K tile row stride (elements)
   constexpr int VROW = KTL + 8;  // V^T tile row stride
   constexpr int NDT = DH / 16;
@@ -229,13 +232,21 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
   const bf16* kb = k + kvb * lk * ldk + h * DH;
   const bf16* vb = v + kvb * lk * ldv + h * DH;
 
-  bf16x8 qf[NQ];
+  bf16x8 qf[NQ];  // K16: the low 4 hold Q[query lr][d = 4 lg .. 4 lg + 3]
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
     const int myq = q0 + (wave * NQ + g) * 16 + lr;
 #pragma unroll
     for (int e = 0; e < 8; ++e) qf[g][e] = (bf16)0.f;
-    if (myq < lq && 8 * lg < DH) qf[g] = *reinterpret_cast<const bf16x8*>(qb + (long)myq * ldq + 8 * lg);
+    if constexpr (K16) {
+      if (myq < lq) {
+        const bf16x4 q4 = *reinterpret_cast<const bf16x4*>(qb + (long)myq * ldq + 4 * lg);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qf[g][e] = q4[e];
+      }
+    } else {
+      if (myq < lq && 8 * lg < DH) qf[g] = *reinterpret_cast<const bf16x8*>(qb + (long)myq * ldq + 8 * lg);
+    }
   }
   if constexpr (DP > DH) {  // K pad columns: zero once, the staging never writes them
     for (int idx = tid; idx < KTL * (DP - DH); idx += 256) {
@@ -285,8 +296,16 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
       f32x4 sacc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(16 * t + lr) * KROW + 8 * lg]);
-        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        if constexpr (K16) {
+          typedef short s4v __attribute__((ext_vector_type(4)));
+          const bf16x4 kf = *reinterpret_cast<const bf16x4*>(&Ks[(16 * t + lr) * KROW + 4 * lg]);
+          const bf16x4 q4 = __builtin_shufflevector(qf[g], qf[g], 0, 1, 2, 3);
+          sacc[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4v, kf), __builtin_bit_cast(s4v, q4),
+                                                              f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        } else {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(16 * t + lr) * KROW + 8 * lg]);
+          sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
       }
       // the running max stays in raw-score units (scale > 0): one fma per score folds the scale
       // and the max subtraction; only the last, partial key tile pays for the mask
@@ -316,11 +335,17 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
       }
       const float mneg = -m_run[g] * scale_log2;
       bf16x8 pf[NS];
+      // the score scaling two at a time (v_pk_fma_f32): this kernel is VALU-bound on the softmax
+      typedef float f2v __attribute__((ext_vector_type(2)));
+      const f2v sc2 = {scale_log2, scale_log2}, mn2 = {mneg, mneg};
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          pf[t >> 1][(t & 1) * 4 + i] = (bf16)__builtin_amdgcn_exp2f(fmaf(sacc[t][i], scale_log2, mneg));
+        for (int i = 0; i < 4; i += 2) {
+          const f2v z = __builtin_elementwise_fma(f2v{sacc[t][i], sacc[t][i + 1]}, sc2, mn2);
+          pf[t >> 1][(t & 1) * 4 + i] = (bf16)__builtin_amdgcn_exp2f(z[0]);
+          pf[t >> 1][(t & 1) * 4 + i + 1] = (bf16)__builtin_amdgcn_exp2f(z[1]);
+        }
 #pragma unroll
       for (int s2 = 0; s2 < NS; ++s2) lsum[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[s2], lsum[g], 0, 0, 0);
       // O^T[d][q] += sum_k V^T[d][key(k)] P^T[key(k)][q]
