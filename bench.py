@@ -46,13 +46,18 @@ def conv_traffic(workload: dict):
     if t.get("workload") != workload:
         return {"bytes_per_launch": None,
                 "reason": f"the committed PMC run measured {t.get('workload')}, not this line's {workload}"}
-    return {"bytes_per_launch": t["bytes_per_launch"], "workload": workload,
-            "source": t.get("source", "profiles/conv_traffic.json")}
+    out = {"bytes_per_launch": t["bytes_per_launch"], "workload": workload,
+           "source": t.get("source", "profiles/conv_traffic.json"), "head": t.get("head")}
+    for k in ("bytes_per_step", "splitk_reduce_bytes_per_step", "splitk_reduce_launches", "launches_counted"):
+        if k in t:
+            out[k] = t[k]
+    return out
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); default: WORLD_SIZE under torch.distributed.run, else 1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=16, help="images per GPU per step (when --global-batch is unset)")
@@ -88,7 +93,32 @@ def parse():
                     help="one-GPU runs with --dtype bf16: also time this many steps of the fp32 parity mode (the "
                          "path whose bitstreams and pixels match the reference) on the same images, and report "
                          "its throughput and the bf16-vs-fp32 bpp / PSNR / MS-SSIM gap; 0 = skip")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def sweep_points(args):
+    """[(target_bpp, rate_gain)] of the run and the headline index: config 4's sweep
+    (--bpp-sweep) or the single config-2 point; the headline (and profiled) point is the one
+    nearest 0.08 bpp."""
+    from rdeic_amd import weights as W
+    if args.bpp_sweep:
+        points = [(float(v), W.rate_gain_for_bpp(float(v))) for v in args.bpp_sweep.split(",")]
+    else:
+        points = [(None, W.RATE_GAIN_BPP008 if args.rate_gain is None else args.rate_gain)]
+    main_i = min(range(len(points)), key=lambda i: abs((points[i][0] or 0.08) - 0.08))
+    return points, main_i
+
+
+def run_sweep(points, main_i, measure):
+    """measure(i, target_bpp, rate_gain, headline) -> result dict for each point, in order. Only the
+    headline point keeps its output images ("out": the fp32 leg compares pixels against them)."""
+    results = []
+    for i, (target, rate_gain) in enumerate(points):
+        r = measure(i, target, rate_gain, i == main_i)
+        if i != main_i:
+            r["out"] = None
+        results.append(r)
+    return results
 
 
 def main():
@@ -110,14 +140,7 @@ def main():
     if B < 1:
         raise SystemExit(f"global batch {G} leaves rank {rank} of {world} without images")
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    from rdeic_amd import weights as W
-    if args.bpp_sweep:
-        targets = [float(v) for v in args.bpp_sweep.split(",")]
-        points = [(t, W.rate_gain_for_bpp(t)) for t in targets]
-    else:
-        points = [(None, W.RATE_GAIN_BPP008 if args.rate_gain is None else args.rate_gain)]
-    # the headline (and profiled) point: config 2's ~0.08 bpp when the sweep holds it
-    main_i = min(range(len(points)), key=lambda i: abs((points[i][0] or 0.08) - 0.08))
+    points, main_i = sweep_points(args)
     model = RDEIC(compute_dtype=dtype, device=dev)
     if args.coder_groups is not None:
         model.preprocess_model.coder_groups = args.coder_groups
@@ -154,8 +177,7 @@ def main():
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
-    results = []
-    for i, (target, rate_gain) in enumerate(points):
+    def measure(i, target, rate_gain, headline):
         log(f"point {i + 1}/{len(points)}: rate_gain {rate_gain}, {args.warmup} warm-up + {args.steps} timed steps, "
             f"{nsess} codec session(s) in flight")
         model.init_synthetic(rate_gain=rate_gain)
@@ -201,7 +223,7 @@ def main():
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         prof = None
-        if i == main_i and not args.no_roofline:
+        if headline and not args.no_roofline:
             # Roofline pass (untimed): the same steps on ONE session with the native launch profiler
             # (HIP events on the launch stream; launches >= 50 GFLOP always, smaller ones 1 in
             # --prof-every), so each kernel's duration is its own and not shared with a concurrent
@@ -220,14 +242,13 @@ def main():
         elapsed = parallel.max_over_ranks(elapsed, dev)
         mrows = metrics.cpu().numpy()
         last_out = sessions[(args.steps - 1) % nsess]._last_out
-        results.append({"target_bpp": target, "rate_gain": rate_gain, "elapsed": elapsed, "prof": prof, "out": last_out,
-                        "mean_bpp": float(mrows[:, 0].mean()), "mean_psnr_db": float(mrows[:, 2].mean()),
-                        "mean_ms_ssim": float(mrows[:, 4].mean()),
-                        "images": int(mrows.shape[0]), "rows": rows_by_step[-1].numpy()})
         del sessions
-        for rr in results:
-            if rr is not results[main_i]:
-                rr.pop("out", None)
+        return {"target_bpp": target, "rate_gain": rate_gain, "elapsed": elapsed, "prof": prof, "out": last_out,
+                "mean_bpp": float(mrows[:, 0].mean()), "mean_psnr_db": float(mrows[:, 2].mean()),
+                "mean_ms_ssim": float(mrows[:, 4].mean()),
+                "images": int(mrows.shape[0]), "rows": rows_by_step[-1].numpy()}
+
+    results = run_sweep(points, main_i, measure)
     fp32_leg = None
     if world == 1 and args.dtype == "bf16" and args.fp32_steps > 0 and not args.bpp_sweep:
         log(f"fp32 parity mode: 1 warm-up + {args.fp32_steps} timed steps on one session, same images")
@@ -289,9 +310,13 @@ def main():
             nb, byts, _ = prof["conv_bytes"]
             roof["algorithmic_bytes_per_launch"] = round(byts / max(1, nb))
             roof["algorithmic_bytes_per_step"] = round(byts / args.steps)
-            tb = roof["traffic"].get("bytes_per_launch") if isinstance(roof["traffic"], dict) else None
-            if tb:
-                roof["traffic_over_algorithmic"] = round(tb / (byts / max(1, nb)), 3)
+            # PMC bytes of the step's conv launches (split-K reduces included) over the library's
+            # algorithmic bytes of the same step: one launch set on both sides (per step, not per launch)
+            tr = roof["traffic"] if isinstance(roof["traffic"], dict) else {}
+            if tr.get("bytes_per_step"):
+                roof["traffic_over_algorithmic"] = round(tr["bytes_per_step"] / (byts / args.steps), 3)
+                roof["traffic_over_algorithmic_excl_splitk_reduce"] = round(
+                    (tr["bytes_per_step"] - tr.get("splitk_reduce_bytes_per_step", 0)) / (byts / args.steps), 3)
         sec = {}
         for kind, v in prof.items():
             if kind in ("conv", "conv_bytes") or kind.startswith("_"):

@@ -336,6 +336,7 @@ int rdeic_prof_start(int32_t capacity, int32_t every);
 #define RDEIC_COUNT_LAYERNORM 2    /* rdeic_layernorm kernels */
 #define RDEIC_COUNT_HALO_SMALL 3   /* the small-image halo conv (UNet / control ResBlocks) */
 #define RDEIC_COUNT_LN_FUSED 4     /* rdeic_layernorm_rowstats (LayerNorm folded into the next linear) */
+#define RDEIC_COUNT_SPLITK 5       /* rdeic_conv2d_splitk launches that ran split (partial pass + reduce) */
 #define RDEIC_COUNT_KINDS 8
 int64_t rdeic_launch_count(int32_t kind);
 /* Per-row LayerNorm statistics (attention.py:273-285, torch.nn.LayerNorm: biased variance, eps) of

@@ -398,6 +398,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.in_hw = (x.shape[1], x.shape[2])
         count_direct_use(weight, ctx.needs_input_grad[1])
         ctx.bias = count_direct_use(bias, ctx.needs_input_grad[2])  # a leaf parameter
+        ctx.splitk = ops.splitk_state()  # the backward runs on autograd's engine thread (ops.splitk_as)
         ctx.save_for_backward(x, weight, z)
         return out
 
@@ -407,8 +408,9 @@ class Conv2dFn(torch.autograd.Function):
         has_emb, has_res, has_bias = ctx.flags
         dout = dout.contiguous()
         nig = ctx.needs_input_grad
-        dx, dw, db, demb = _conv_backward(x, weight, z, dout, ctx.cfg, ctx.in_hw, nig[0], nig[1],
-                                          has_bias and nig[2], has_emb and nig[3], bias=ctx.bias)
+        with ops.splitk_as(ctx.splitk):
+            dx, dw, db, demb = _conv_backward(x, weight, z, dout, ctx.cfg, ctx.in_hw, nig[0], nig[1],
+                                              has_bias and nig[2], has_emb and nig[3], bias=ctx.bias)
         return dx, dw, db, demb, (dout if has_res else None), None
 
 
@@ -433,6 +435,7 @@ class LinearFn(torch.autograd.Function):
         ctx.flags = (res is not None, bias is not None)
         count_direct_use(weight, ctx.needs_input_grad[1])
         ctx.bias = count_direct_use(bias, ctx.needs_input_grad[2])
+        ctx.splitk = ops.splitk_state()
         ctx.save_for_backward(x, weight)
         return out.view(rows, weight.shape[0])
 
@@ -443,8 +446,9 @@ class LinearFn(torch.autograd.Function):
         dout = dout.contiguous()
         rows = x.shape[0]
         nig = ctx.needs_input_grad
-        dx, dw, db, _ = _conv_backward(_tok4(x), weight, None, _tok4(dout), ctx.cfg, (rows, 1), nig[0], nig[1],
-                                       has_bias and nig[2], False, bias=ctx.bias)
+        with ops.splitk_as(ctx.splitk):
+            dx, dw, db, _ = _conv_backward(_tok4(x), weight, None, _tok4(dout), ctx.cfg, (rows, 1), nig[0], nig[1],
+                                           has_bias and nig[2], False, bias=ctx.bias)
         if dx is not None:
             dx = dx.view(rows, weight.shape[1])
         return dx, dw, db, (dout if has_res else None), None

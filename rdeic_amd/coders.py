@@ -102,8 +102,9 @@ def default_threads() -> int:
     """Host coder threads per call, at most 16. RDEIC_CODER_THREADS overrides. Otherwise: the CPUs
     this process may run on (affinity set), capped by the cgroup CPU quota (a GPU box shows 256 CPUs
     but grants 16). The quota is shared by every rank of this node (LOCAL_WORLD_SIZE, one process
-    per GPU), so each rank takes quota / LWS; the affinity set is divided the same way only when it is
-    node-wide — a launcher that binds each rank to its own cores has already split it."""
+    per GPU), so each rank takes quota / LWS. The affinity set is divided the same way unless the
+    launcher says it bound each rank to its own cores (RDEIC_RANK_BOUND=1): a cpuset-limited container
+    also shows fewer CPUs than os.cpu_count(), and its ranks share that set."""
     env = os.environ.get("RDEIC_CODER_THREADS")
     if env:
         return max(1, int(env))
@@ -115,8 +116,7 @@ def default_threads() -> int:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
-    node = os.cpu_count() or aff
-    n = aff // lws if aff >= node else aff
+    n = aff if os.environ.get("RDEIC_RANK_BOUND") == "1" else aff // lws
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
             quota, period = f.read().split()[:2]

@@ -2293,6 +2293,7 @@ extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, flo
     ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
     rc = conv2d_splitk_impl(d, splits, ws, ws_floats, stream);
   }
+  if (rc == RDEIC_OK) rdeic_count_launch(RDEIC_COUNT_SPLITK);
   if (rc != RDEIC_OK || !d->gn_part) return rc;  // statistics of the reduced output: stand-alone pass
   return gn_rows_partial(d->out, (long)d->n * d->ho * d->wo, d->cout, d->out_ld, d->gn_hw, d->gn_part,
                          d->out_f32 ? 0 : 1, (hipStream_t)stream);

@@ -45,12 +45,16 @@ def visible_gpus() -> int:
     return int(torch.cuda.device_count())
 
 
-def role(nproc: int) -> str:
+def role(nproc: Optional[int]) -> str:
     """'rank' when the environment already makes this process one rank of a job (or nproc == 1),
-    'launcher' when it must start nproc ranks itself. Refuses a WORLD_SIZE that disagrees with nproc."""
+    'launcher' when it must start nproc ranks itself. nproc None (--gpus not given): the environment's
+    WORLD_SIZE when set (plain `torch.distributed.run --nproc-per-node N script`), else 1. An explicit
+    nproc that disagrees with WORLD_SIZE is refused."""
+    ws = os.environ.get("WORLD_SIZE")
+    if nproc is None:
+        return "rank"
     if nproc < 1:
         raise LaunchError(f"--gpus must be >= 1, got {nproc}")
-    ws = os.environ.get("WORLD_SIZE")
     if ws is not None:
         if int(ws) != nproc:
             raise LaunchError(f"WORLD_SIZE={ws} in the environment disagrees with --gpus {nproc}")
@@ -119,7 +123,7 @@ def spawn(nproc: int, script: str, argv: List[str], *, require_gpus: bool = True
     return status
 
 
-def maybe_launch(nproc: int, script: str, argv: Optional[List[str]] = None, **kw) -> None:
+def maybe_launch(nproc: Optional[int], script: str, argv: Optional[List[str]] = None, **kw) -> None:
     """Call first thing in a `--gpus N` script, before anything touches the GPU: returns when this
     process is a rank; otherwise runs the job as its launcher and exits with the job's status."""
     if role(nproc) == "rank":

@@ -342,6 +342,25 @@ class splitk_allowed:
         _SPLITK_TLS.allowed, _SPLITK_TLS.short = self._prev
 
 
+class splitk_as:
+    """Context manager restoring a captured splitk_state() on the calling thread. PyTorch runs the
+    backward of autograd Functions on its own per-device engine thread, whose switches are the
+    defaults (off): Conv2dFn / LinearFn capture the forward thread's state in ctx and re-enter it
+    around their backward convs, so the input gradients of a training step split K as the forward
+    did (finetune.py's splitk_allowed(short_k=True))."""
+
+    def __init__(self, state):
+        self.state = tuple(state)
+
+    def __enter__(self):
+        self._prev = splitk_state()
+        _SPLITK_TLS.allowed, _SPLITK_TLS.short = self.state
+        return self
+
+    def __exit__(self, *exc):
+        _SPLITK_TLS.allowed, _SPLITK_TLS.short = self._prev
+
+
 def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor, n: int) -> int:
     """Number of k-splits (1 = none): only when the 128x128 tile grid cannot fill the chip.
     Inference: a function of the per-image M only (SPLITK_NOMINAL_BATCH); n = images in the launch."""
@@ -505,7 +524,7 @@ HALO_MAX_C = 512
 
 
 # launch counters of the library (rdeic_launch_count, RDEIC_COUNT_* in include/rdeic_hip.h)
-COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED = 0, 1, 2, 3, 4
+COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED, COUNT_SPLITK = 0, 1, 2, 3, 4, 5
 
 
 def launch_count(kind: int) -> int:

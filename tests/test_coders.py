@@ -233,13 +233,15 @@ def test_default_threads_shared_among_local_ranks(monkeypatch):
 
 
 def test_default_threads_respects_per_rank_binding(monkeypatch):
-    """A launcher that binds each rank to its own cores has already split the CPUs: the affinity set is
-    not divided again, and RDEIC_CODER_THREADS overrides everything."""
+    """The affinity set is divided among the node's ranks unless the launcher declares per-rank binding
+    (RDEIC_RANK_BOUND=1): a cpuset-limited container (affinity < os.cpu_count(), no quota) is shared by
+    every rank, and RDEIC_CODER_THREADS overrides everything."""
     import os
     monkeypatch.delenv("RDEIC_CODER_THREADS", raising=False)
+    monkeypatch.delenv("RDEIC_RANK_BOUND", raising=False)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
-    monkeypatch.setattr(os, "cpu_count", lambda: 64)
-    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(6)), raising=False)
+    monkeypatch.setattr(os, "cpu_count", lambda: 256)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)), raising=False)
     import builtins
     real_open = builtins.open
 
@@ -248,8 +250,10 @@ def test_default_threads_respects_per_rank_binding(monkeypatch):
             raise OSError("no cgroup")
         return real_open(path, *a, **k)
     monkeypatch.setattr(builtins, "open", no_quota)
-    assert coders.default_threads() == 6          # bound per rank: 6 own cores, not 6 // 8
-    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(64)), raising=False)
-    assert coders.default_threads() == 8          # node-wide affinity: 64 // 8
+    assert coders.default_threads() == 8          # cpuset of 64 shared by 8 ranks, not 8 x 16
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(6)), raising=False)
+    assert coders.default_threads() == 1          # 6 // 8, at least one
+    monkeypatch.setenv("RDEIC_RANK_BOUND", "1")
+    assert coders.default_threads() == 6          # bound per rank: 6 own cores
     monkeypatch.setenv("RDEIC_CODER_THREADS", "3")
     assert coders.default_threads() == 3

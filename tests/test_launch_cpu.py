@@ -54,3 +54,45 @@ def test_bench_refuses_more_gpus_than_visible():
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "needs 2 visible GPUs" in r.stderr
     assert r.stdout.strip() == ""
+
+
+BENCH_STUB = os.path.join(ROOT, "tests", "stubs", "bench_stub.py")
+
+
+def test_config4_command_eight_ranks():
+    """Config 4's exact command (`bench.py --gpus 8 --global-batch 128 --bpp-sweep 0.04,0.08,0.12`) through
+    bench.py's own parser, launcher, sharding and sweep handling (gloo stub step): 8 ranks, one line,
+    16 images per rank in global order, and the headline point (0.08, index 1: not the first point; the
+    r04 sweep crashed there) is the only one that keeps its output images."""
+    r = subprocess.run([sys.executable, BENCH_STUB, "--gpus", "8", "--global-batch", "128",
+                        "--bpp-sweep", "0.04,0.08,0.12"], capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["global_batch"] == 128
+    assert d["targets"] == [0.04, 0.08, 0.12] and d["main_i"] == 1
+    assert d["images_per_point"] == [128, 128, 128]
+    assert d["image_order"] == list(range(128))
+    assert d["rank_of_image"] == [g // 16 for g in range(128)]  # 16 images per rank, contiguous shards
+    assert d["out_kept"] == [False, True, False]
+    assert d["rate_gains"][0] < d["rate_gains"][1] < d["rate_gains"][2]
+
+
+def test_torchrun_form_without_gpus_flag():
+    """`torch.distributed.run --nproc-per-node N bench.py` without --gpus: the rank takes WORLD_SIZE from the
+    environment (the --gpus default of 1 used to refuse it)."""
+    from rdeic_amd import launch
+    env = _env()
+    env.update(WORLD_SIZE="4", RANK="0", LOCAL_RANK="0")
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        os.environ.update({k: env[k] for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+        assert launch.role(None) == "rank"
+        assert launch.role(4) == "rank"
+    finally:
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+            if old[k] is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = old[k]

@@ -285,3 +285,30 @@ def test_pack_batch_matches_single_packs(gpu, dt):
                 assert sp.lookup(w, dt, mode) is not None
     for (w, packed, *_), ref in zip(sp.jobs, refs):
         assert torch.equal(packed, ref)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_backward_keeps_forward_splitk(gpu, dt):
+    """autograd runs Conv2dFn.backward on its own engine thread, whose split-K
+    switches are off, so the B=1 input-gradient convs of the fine-tune step stopped splitting K.
+    The backward now re-enters the forward thread's state (ops.splitk_as): under
+    splitk_allowed(short_k=True) the 8x8 1280-channel dgrad conv must run split, and match torch."""
+    from rdeic_amd import autograd as AG, ops
+    g = torch.Generator(device="cuda").manual_seed(5)
+    cin = cout = 1280
+    x = torch.randn((1, cin, 8, 8), device="cuda", generator=g)
+    W = torch.randn((cout, cin, 3, 3), device="cuda", generator=g) / math.sqrt(cin * 9)
+    gout = torch.randn((1, cout, 8, 8), device="cuda", generator=g)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, W, None, padding=1).backward(gout)
+    xn = _nhwc(x).to(dt).requires_grad_(True)
+    Wo = W.clone()  # frozen fp32 master (the UNet's), packed in the compute dtype: only the input gradient
+    cfg = AG.ConvCfg(3, 3, 1, 1)
+    with ops.splitk_allowed(short_k=True):
+        out = AG.conv2d(xn, Wo, None, cfg=cfg)
+        ops.launch_count_reset()
+        out.backward(_nhwc(gout).to(dt))
+        torch.cuda.synchronize()
+    assert ops.launch_count(ops.COUNT_SPLITK) >= 1
+    assert ops.splitk_state() == (False, False)  # nothing leaked into this thread
+    assert _rel(_nchw(xn.grad.float()), xr.grad) < (1e-5 if dt == torch.float32 else 2e-2)

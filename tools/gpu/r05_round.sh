@@ -1,15 +1,15 @@
 #!/bin/bash
-# r04 end-of-session validation in ONE call: the driver's gpu tests, smoke, the default bench line,
+# r05 validation (RDEIC_HEAD=<commit> names the tree in the profiles) in ONE call: the driver's gpu tests, smoke, the default bench line,
 # a rocprofv3 kernel trace of the bench (step slice + conv cross-check), and the PMC HBM traffic passes.
-# usage (repo root on the box): bash tools/gpu/r04_round.sh TAG
+# usage (repo root on the box): RDEIC_HEAD=$(git rev-parse --short HEAD) bash tools/gpu/r05_round.sh TAG
 set -o pipefail
-TAG=${1:-r04_final}
+TAG=${1:-r05_final}
 R=$PWD
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -m pytest tests/ -x -q -m gpu > $O/pytest.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest.log; exit 4; }
-tail -1 $O/pytest.log
+timeout -k 10 900 python3 -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest.log; exit 4; }
+grep -E "passed|failed" $O/pytest.log | tail -1
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 6; }
 tail -1 $O/smoke.log
 timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 5; }

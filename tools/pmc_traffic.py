@@ -51,11 +51,20 @@ w_tot, w_cnt, _ = per_kernel(os.path.join(out_dir, "write", "**", "*counter_coll
 launches = sum(f_cnt.values())
 fetch_b = 2 * sum(f_tot.values()) * 1024
 write_b = sum(w_tot.values()) * 1024
+red = [k for k in f_tot if "splitk_reduce" in k]
+red_b = sum(2 * f_tot[k] * 1024 + w_tot.get(k, 0) * 1024 for k in red)
 print(json.dumps({
+    # per step (the one timed bench step the passes cover): the figure bench.py divides by the library's
+    # algorithmic bytes of the same step (both cover every conv launch of the step; the split-K reduce
+    # launches have no algorithmic bytes of their own and are also reported apart)
+    "bytes_per_step": round(fetch_b + write_b),
+    "splitk_reduce_bytes_per_step": round(red_b),
+    "splitk_reduce_launches": sum(f_cnt[k] for k in red),
     "bytes_per_launch": round((fetch_b / max(1, launches)) + write_b / max(1, sum(w_cnt.values()))),
     "fetch_bytes_per_launch": round(fetch_b / max(1, launches)),
     "write_bytes_per_launch": round(write_b / max(1, sum(w_cnt.values()))),
     "launches_counted": launches,
+    "head": os.environ.get("RDEIC_HEAD"),  # the commit the passes ran (set by the GPU round script)
     "workload": workload(sys.argv[2:]),
     "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 1 --warmup 1, timed step only "
               "(tools/pmc_bench.sh)",

@@ -153,7 +153,9 @@ def main():
     ap.add_argument("--bench", help="bench JSON line of the same profiled run")
     ap.add_argument("--out")
     a = ap.parse_args()
-    summ = {"source": a.trace.split("gpurun_out/")[-1], "step": "last timed step (image_mse_kernel-delimited)"}
+    import os
+    summ = {"source": a.trace.split("gpurun_out/")[-1], "head": os.environ.get("RDEIC_HEAD"),
+            "step": "last timed step (image_mse_kernel-delimited)"}
     summ.update(summarise(last_step(load(a.trace))))
     if a.bench:
         with open(a.bench) as f:
