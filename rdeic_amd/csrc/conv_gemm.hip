@@ -1425,33 +1425,6 @@ __device__ unsigned long long* g_halo_stamps;
 #else
 #define HALO_STAMP(k) do {} while (0)
 #endif
-// diagnostic build only: RDEIC_HALO_DIAG bits remove one mechanism of the main loop (results wrong,
-// timing tells what bounds it): 1 per-tap DMA waits, 2 per-tap barriers, 4 MFMAs, 8 GroupNorm transform
-#ifndef RDEIC_HALO_DIAG
-#define RDEIC_HALO_DIAG 0
-#endif
-#ifndef RDEIC_HALO8_SPREAD
-#define RDEIC_HALO8_SPREAD 3  // A/B build switch (tools/halo_stamps.hip): see conv3x3_halo8_kernel; 3 measured best (r04)
-#endif
-#ifndef RDEIC_HALO8_VMFAST
-#define RDEIC_HALO8_VMFAST 1  // A/B build switch: compile-time vmcnt in the weight waves' steady state
-#endif
-#ifndef RDEIC_HALO8_LAUNDER
-#define RDEIC_HALO8_LAUNDER 1  // A/B build switch: recompute the transform's offsets in the loop (no scratch)
-#endif
-#ifndef RDEIC_HALO8_PRIO
-#define RDEIC_HALO8_PRIO 0  // A/B build switch: s_setprio(1) around each tap's MFMA cluster
-#endif
-#ifndef RDEIC_HALO8_HSPLIT
-#define RDEIC_HALO8_HSPLIT 1  // A/B build switch: the next halo issued in two halves (taps 0 and 2); measured -0.3..0.9% cycles (r04q)
-#endif
-#ifndef RDEIC_HALO8_TW
-#define RDEIC_HALO8_TW 4  // A/B build switch: the tap at which the next halo is waited for (transform: taps TW..TW+2); 4 measured best (r04o)
-#endif
-#ifndef RDEIC_HALO8_BAR2
-#define RDEIC_HALO8_BAR2 1  // A/B build switch: one barrier per two taps in conv3x3_halo8_kernel (default, r04)
-#endif
-
 // GN: 0 plain conv, 1 GroupNorm affine on the input, 2 affine + SiLU (compile-time: no per-element branch);
 // FE: the fast epilogue (halo_epilogue: bf16 out, no emb / activation), else epilogue_vec
 template <int GN, bool FE>
@@ -1605,9 +1578,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     for (int t = 0; t < 9; ++t) {
       // this tap's weights (and at tap 2 the next halo); younger ops allowed in flight: the next tap's
       // weights and, at tap 1, the next halo's 4 pieces issued at tap 0
-      if (RDEIC_HALO_DIAG & 1) {
-        if (t == 8 && !more) wait_vm<0>();
-      } else if (t == 1) {
+      if (t == 1) {
         if (more) wait_vm<5>(); else wait_vm<1>();
       } else if (t < 8 || more) {
         wait_vm<1>();
@@ -1616,7 +1587,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       } else {
         wait_vm<0>();
       }
-      if (!(RDEIC_HALO_DIAG & 2)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
       if (t + 2 < 9) {
         dma16(rsw, bbuf + ((t + 2) % NB) * BBYTES + wave * 1024, bvo, ((t + 2) * cin + cb * 32) * 2);
       } else if (more) {
@@ -1640,17 +1611,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int i = 0; i < 4; ++i) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (RDEIC_HALO_DIAG & 4)
-            asm volatile("" ::"v"(af), "v"(bfv[j]));
-          else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
       }
       // the next block's halo (own pieces landed at tap 2's wait) is transformed one piece per tap over
       // taps 2..5, AFTER this tap's MFMAs are issued, so its VALU runs beside the matrix pipe instead of
       // delaying the next barrier; the block reads it from its tap 0 on (several barriers later)
-      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
+      if constexpr (GN != 0)
         if (t >= 2 && t < 6 && more) {
           transform_piece(cb + 1, t - 2);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier
@@ -1759,8 +1725,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
 
   // halo waves: pieces hw + 8 k (k < 6; past the 42 pieces, piece hw + 32 again: same bytes, same slots).
   // A piece's source offset (or out-of-image zeros) is recomputed at each issue from a laundered lane id
-  // (six live offsets would push the 128-VGPR loop into scratch); hinfo keeps, per piece, a valid bit
-  // (real piece, inside the image: transform it) and the lane's logical channel chunk (bits 8 + 2k).
+  // (six live offsets would push the 128-VGPR loop into scratch).
   auto hpiece = [&](int k) { return hw + 8 * k < NPIECE ? hw + 8 * k : hw + 32; };  // wave-uniform
   auto halo_voff = [&](int k, int ln) {
     const int p = hpiece(k);
@@ -1774,45 +1739,31 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     }
     return vo;
   };
-  unsigned hinfo = 0;
-  if (!wload && RDEIC_HALO8_SPREAD != 3) {
-#pragma unroll
-    for (int k = 0; k < PPW; ++k) {
-      const int sl = hpiece(k) * 16 + (lane >> 2);
-      if (hw + 8 * k < NPIECE && halo_voff(k, lane) != kOOB) hinfo |= 1u << k;
-      hinfo |= (unsigned)((lane & 3) ^ sw(sl)) << (8 + 2 * k);
-    }
-  }
   auto hpo = [&](int k) { return hpiece(k) * 1024; };
-  // RDEIC_HALO8_SPREAD == 3: the transform is balanced over all 16 waves, wave w taking pieces
-  // w + 16 k (k < 3, < 42) whoever loaded them; tinfo: per k a valid bit (bit k) and the chunk (bits 8 + 2k)
+  // The GroupNorm transform is balanced over all 16 waves: wave w transforms pieces w + 16 k (k < 3,
+  // < 42) whoever loaded them (r04: -3.5% against transforming by the loader). tinfo: per k a valid bit
+  // (bit k: a real piece inside the image) and the lane's logical channel chunk (bits 8 + 2k).
   unsigned tinfo = 0;
-  if (RDEIC_HALO8_SPREAD == 3) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int p = wave + 16 * k;
-      const int sl = p * 16 + (lane >> 2), ph = lane & 3;
-      bool in = false;
-      if (p < NPIECE && sl < HPIX) {
-        const int hr = sl / HC, hc = sl - (sl / HC) * HC;
-        const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
-        in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      }
-      if (in) tinfo |= 1u << k;
-      tinfo |= (unsigned)(ph ^ sw(sl)) << (8 + 2 * k);
+  for (int k = 0; k < 3; ++k) {
+    const int p = wave + 16 * k;
+    const int sl = p * 16 + (lane >> 2), ph = lane & 3;
+    bool in = false;
+    if (p < NPIECE && sl < HPIX) {
+      const int hr = sl / HC, hc = sl - (sl / HC) * HC;
+      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+      in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
     }
+    if (in) tinfo |= 1u << k;
+    tinfo |= (unsigned)(ph ^ sw(sl)) << (8 + 2 * k);
   }
-  auto issue_halo_piece = [&](int cb, int k) {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    dma16(rs0, hbuf + (cb & 1) * HBYTES + hpo(k), halo_voff(k, ln), cb * 64);
-  };
-  auto issue_halo = [&](int cb) {
+  // halo waves: all six pieces of block cb (prologue), or half of them (main loop, k in [k0, k1))
+  auto issue_halo = [&](int cb, int k0, int k1) {
     char* dst = hbuf + (cb & 1) * HBYTES;
     int ln = lane;
     asm volatile("" : "+v"(ln));
 #pragma unroll
-    for (int k = 0; k < PPW; ++k) dma16(rs0, dst + hpo(k), halo_voff(k, ln), cb * 64);
+    for (int k = k0; k < k1; ++k) dma16(rs0, dst + hpo(k), halo_voff(k, ln), cb * 64);
   };
   // weight waves: rows n = 16 wave + lane / 4, chunk lane % 4 of every tap slice
   unsigned bvo = kOOB;
@@ -1824,38 +1775,30 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     const int cb = u / 9, t = u - (u / 9) * 9;
     dma16(rsw, bbuf + (u % NB) * BBYTES + wave * 1024, bvo, (t * cin + cb * 32) * 2);
   };
-  // piece k of a halo wave's pieces of block cb, in place (skipped: duplicates and out-of-image chunks);
-  // SPREAD == 3: piece wave + 16 k of the block, whoever loaded it
+  // piece wave + 16 k of block cb, in place (out-of-image chunks stay zero: the conv's padding of the
+  // normalised tensor). info and lane are laundered so their derived offsets are recomputed here instead of
+  // hoisted out of the channel-block loop, where hipcc kept them in scratch; every reload was an
+  // s_waitcnt vmcnt(0) that drained the weight ring's in-flight LDS-DMA (r04)
   auto transform_piece = [&](int cb, int k) {
-    // info and lane laundered: their derived offsets are recomputed here instead of hoisted out of the
-    // channel-block loop, where hipcc kept them in scratch; every reload was an s_waitcnt vmcnt(0)
-    // that drained the weight ring's in-flight LDS-DMA (r04)
-    unsigned info = RDEIC_HALO8_SPREAD == 3 ? tinfo : hinfo;
+    unsigned info = tinfo;
     int ln = lane;
-    if (RDEIC_HALO8_LAUNDER) asm volatile("" : "+v"(info), "+v"(ln));
+    asm volatile("" : "+v"(info), "+v"(ln));
     if (!(info & (1u << k))) return;
-    char* pc = hbuf + (cb & 1) * HBYTES + ln * 16 + (RDEIC_HALO8_SPREAD == 3 ? (wave + 16 * k) * 1024 : hpo(k));
-    {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(pc);
-      const int ch = (info >> (8 + 2 * k)) & 3;
-      const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
-      const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
-      const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
-      const float bv[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
-      bf16x8 o;
+    char* pc = hbuf + (cb & 1) * HBYTES + ln * 16 + (wave + 16 * k) * 1024;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(pc);
+    const int ch = (info >> (8 + 2 * k)) & 3;
+    const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
+    const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
+    const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+    const float bv[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+    bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = __builtin_fmaf((float)v[e], av[e], bv[e]);
-        if constexpr (GN == 2) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
-        o[e] = (bf16)x;
-      }
-      *reinterpret_cast<bf16x8*>(pc) = o;
+    for (int e = 0; e < 8; ++e) {
+      float x = __builtin_fmaf((float)v[e], av[e], bv[e]);
+      if constexpr (GN == 2) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+      o[e] = (bf16)x;
     }
-  };
-  auto transform = [&](int cb) {  // halo waves: all their real pieces of block cb
-#pragma unroll 1
-    for (int k = 0; k < PPW; ++k) transform_piece(cb, k);  // one piece at a time (register budget)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
+    *reinterpret_cast<bf16x8*>(pc) = o;
   };
 
   f32x4 acc[4][4];
@@ -1876,122 +1819,74 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
           (void*)(a.gn_ab + (long)img * cin * 2), (short)0, tbytes, 0x00020000);
       dma16(rst, reinterpret_cast<char*>(abl) + tp * 1024, (unsigned)(tp * 1024 + lane * 16), 0);
     }
-    issue_halo(0);
+    issue_halo(0, 0, PPW);
     wait_vm<0>();
   }
   if constexpr (GN != 0) {
-    __syncthreads();  // every table piece (and, for SPREAD == 3, every halo piece) has landed
-    if (!wload || RDEIC_HALO8_SPREAD == 3) transform(0);
+    __syncthreads();  // every table piece and every halo piece of block 0 has landed
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) transform_piece(0, k);  // one piece at a time (register budget)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
   }
 
   HALO_STAMP(1);
   const int lr = lane & 15, lq = lane >> 4;
   const int bsw = (lq ^ sw(lr)) * 16;
+  // Schedule (r04, each step measured): one barrier per two taps, every wait and weight
+  // DMA issue at even taps; the next halo issued in two halves at taps 0 and 2, waited for at tap 4 and
+  // transformed at taps 4..6 after each tap's MFMAs.
   for (int cb = 0; cb < ncb; ++cb) {
     const bool more = cb + 1 < ncb;
     const char* hb = hbuf + (cb & 1) * HBYTES;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int u = cb * 9 + t;
-      // BAR2: barriers (and every wait and DMA issue) only at even taps of a channel block; the odd tap
-      // after one reads the slice the same barrier published
-      const bool BAR = !RDEIC_HALO8_BAR2 || (t % 2 == 0);  // t is unrolled: a compile-time value
-      if (RDEIC_HALO_DIAG & 1) {
-        if (t == 8 && !more) wait_vm<0>();
-      } else if (RDEIC_HALO8_BAR2) {
-        if (wload && BAR) {  // slices u and (t < 8) u + 1 landed; issued so far: up to u + 5
+      const bool BAR = t % 2 == 0;  // t is unrolled: a compile-time value
+      if (wload && BAR) {  // slices u and (t < 8) u + 1 landed; issued so far: up to u + 5
+        if (u + 6 < U) {
+          t < 8 ? wait_vm<4>() : wait_vm<5>();  // steady state: a compile-time count, no branch chain
+        } else {
           const int issued = u + 5 < U - 1 ? u + 5 : U - 1;
           const int need = (t < 8 && u + 1 < U) ? u + 1 : u;
-          if (RDEIC_HALO8_VMFAST && u + 6 < U)
-            t < 8 ? wait_vm<4>() : wait_vm<5>();  // steady state: a compile-time count (t is unrolled), no branch chain
-          else
-            wait_vm_rt(issued - need);
-        }
-      } else if (wload) {  // slice u landed; younger: the slices issued after it (and at the last tap the residual)
-        const int ahead = U - 1 - u < LEAD - 1 ? U - 1 - u : LEAD - 1;
-        wait_vm_rt(ahead + (res_dma && u == U - 1 ? 2 : 0));
-      } else if (t == 8 && !more && res_dma) {
-        wait_vm<2>();  // nothing of the halo stream is outstanding (the residual is younger)
-      }
-      if (!wload && more && !(RDEIC_HALO_DIAG & 1)) {  // this wave's pieces of the next block have landed
-        if (RDEIC_HALO8_SPREAD == 2) {
-          if (t >= 2 && t < 2 + PPW) {  // piece t - 2 (issued two taps ago); younger: piece t - 1 if issued
-            if (t - 1 < PPW) wait_vm<1>(); else wait_vm<0>();
-          }
-        } else if (t == RDEIC_HALO8_TW) {  // all six (issued at tap 0)
-          wait_vm<0>();
+          wait_vm_rt(issued - need);
         }
       }
-      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8))
-        if (RDEIC_HALO8_SPREAD == 0 && t == 2 && more && !wload) transform(cb + 1);
-      if (!(RDEIC_HALO_DIAG & 2) && BAR) __builtin_amdgcn_s_barrier();
-      if (RDEIC_HALO_DIAG & 32) {  // diag: no DMA issued in the main loop
-      } else if (wload) {
-        if (RDEIC_HALO8_BAR2) {
-          if (BAR) {  // slices u + 6 and (t < 8) u + 7: slots last read at taps u - 2 and u - 1
-            if (u + LEAD < U) issue_b(u + LEAD);
-            if (t < 8 && u + LEAD + 1 < U) issue_b(u + LEAD + 1);
-          }
-        } else if (u + LEAD < U) {
-          issue_b(u + LEAD);
+      if (!wload && more && t == 4) wait_vm<0>();  // this wave's six pieces of the next block have landed
+      if (BAR) __builtin_amdgcn_s_barrier();
+      if (wload) {
+        if (BAR) {  // slices u + 6 and (t < 8) u + 7: slots last read at taps u - 2 and u - 1
+          if (u + LEAD < U) issue_b(u + LEAD);
+          if (t < 8 && u + LEAD + 1 < U) issue_b(u + LEAD + 1);
         }
-      } else if (RDEIC_HALO8_SPREAD == 2) {
-        if (t < PPW && more) issue_halo_piece(cb + 1, t);  // piece t, transformed at tap t + 2
-      } else if (RDEIC_HALO8_HSPLIT && RDEIC_HALO8_TW >= 4 && (t == 0 || t == 2) && more) {
-        // the next halo's six pieces in two halves (taps 0 and 2), so no barrier waits on a wave issuing six
-        char* dst = hbuf + ((cb + 1) & 1) * HBYTES;
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-#pragma unroll
-        for (int k = (t == 0 ? 0 : PPW / 2); k < (t == 0 ? PPW / 2 : PPW); ++k)
-          dma16(rs0, dst + hpo(k), halo_voff(k, ln), (cb + 1) * 64);
-      } else if (t == 0 && more) {
-        issue_halo(cb + 1);
+      } else if (t == 0 && more) {  // the next halo's six pieces in two halves, so no barrier waits on six
+        issue_halo(cb + 1, 0, PPW / 2);
+      } else if (t == 2 && more) {
+        issue_halo(cb + 1, PPW / 2, PPW);
       }
-      if (t == (RDEIC_HALO8_BAR2 ? 8 : 7) && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
+      if (t == 8 && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
         halo_res_dma<NW>(rsr, lds + res_off(f, 0), (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
       const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
       const int ky = t / 3, kx = t - (t / 3) * 3;
       bf16x8 bfv[4];
-      using i32x4d = int __attribute__((ext_vector_type(4)));
-      int zq = lane;  // diag 16: fragments from registers, no LDS reads
-      if (RDEIC_HALO_DIAG & 16) asm volatile("" : "+v"(zq));
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bfv[j] = (RDEIC_HALO_DIAG & 16) ? __builtin_bit_cast(bf16x8, (i32x4d{zq, zq + j, zq ^ j, zq + 7}))
-                                        : *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
+      for (int j = 0; j < 4; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
       int lb = wm * HC + lr;
       asm volatile("" : "+v"(lb));
       const int sl = lb + ky * HC + kx;
       const char* ab = hb + sl * 64 + ((lq ^ sw(sl)) << 4);
-      if (RDEIC_HALO8_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bf16x8 af = (RDEIC_HALO_DIAG & 16) ? __builtin_bit_cast(bf16x8, (i32x4d{zq + i, zq, zq - i, zq}))
-                                                 : *reinterpret_cast<const bf16x8*>(ab + i * 1024);
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (RDEIC_HALO_DIAG & 4)
-            asm volatile("" ::"v"(af), "v"(bfv[j]));
-          else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
       }
-      if (RDEIC_HALO8_PRIO) __builtin_amdgcn_s_setprio(0);
-      // RDEIC_HALO8_SPREAD 1 / 2: the next block's transform one piece per tap over taps 2..7 by its loader,
-      // after this tap's MFMAs in program order (its VALU beside the matrix pipe, not in front of the
-      // barrier); 3: pieces wave + 16 k, k = 0..2, by every wave at taps 2..4 (the loaders' tap-2 wait and
-      // barrier made them visible)
-      if constexpr (GN != 0 && !(RDEIC_HALO_DIAG & 8)) {
-        if ((RDEIC_HALO8_SPREAD == 1 || RDEIC_HALO8_SPREAD == 2) && t >= 2 && t < 2 + PPW && more && !wload) {
-          transform_piece(cb + 1, t - 2);
+      // the next block's transform: pieces wave + 16 k, k = 0..2, by every wave at taps 4..6 (the loaders'
+      // tap-4 wait and barrier made them visible), after this tap's MFMAs in program order
+      if constexpr (GN != 0)
+        if (t >= 4 && t < 7 && more) {
+          transform_piece(cb + 1, t - 4);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier
         }
-        if (RDEIC_HALO8_SPREAD == 3 && t >= RDEIC_HALO8_TW && t < RDEIC_HALO8_TW + 3 && more) {
-          transform_piece(cb + 1, t - RDEIC_HALO8_TW);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-      }
     }
   }
   HALO_STAMP(2);
