@@ -124,6 +124,9 @@ int rdeic_set_conv_path(int32_t path);
  * key 9: the halo conv's 8-row form (one 1024-thread block per CU, 8-slot weight ring) where the
  *        output height is a multiple of 8 and the epilogue is bf16 without emb / activation: 1 on
  *        (default), 0 the 4-row form everywhere (bit-identical outputs);
+ * key 10: the halo conv's 256-channel form (4 x 64 pixels x 256 channels per 1024-thread block) where
+ *        cout % 256 == 0 and the epilogue is bf16 without emb / activation: 1 on (default), 0 off
+ *        (bit-identical outputs);
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way
  * (keys 0-5; 6 and 8 change fp32 rounding only). */
 int rdeic_set_conv_option(int32_t key, int32_t value);
@@ -337,6 +340,7 @@ int rdeic_prof_start(int32_t capacity, int32_t every);
 #define RDEIC_COUNT_HALO_SMALL 3   /* the small-image halo conv (UNet / control ResBlocks) */
 #define RDEIC_COUNT_LN_FUSED 4     /* rdeic_layernorm_rowstats (LayerNorm folded into the next linear) */
 #define RDEIC_COUNT_SPLITK 5       /* rdeic_conv2d_splitk launches that ran split (partial pass + reduce) */
+#define RDEIC_COUNT_HALO256 6      /* conv3x3_halo256_kernel (the 256-channel halo conv, cout % 256 == 0) */
 #define RDEIC_COUNT_KINDS 8
 int64_t rdeic_launch_count(int32_t kind);
 /* Per-row LayerNorm statistics (attention.py:273-285, torch.nn.LayerNorm: biased variance, eps) of

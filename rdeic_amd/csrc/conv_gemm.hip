@@ -1895,6 +1895,365 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
   HALO_STAMP(3);
 }
 
+// ============================================================================================
+// The 256-channel halo conv (r05): one 1024-thread block per CU computes 4 x 64 output pixels x 256
+// channels (16 waves: 4 output rows x 4 channel quarters of 64, the same 64 x 64 wave tile and MFMA order
+// as the 4- and 8-row kernels, so outputs and statistics are bit-identical to them). Against halo8 (8 x 64
+// pixels x 128 channels) it stages and transforms 396 halo pixels per channel block instead of 660 for the
+// same MFMA work: the GroupNorm + SiLU transform per output falls by 40% on the cout >= 256 layers, at the
+// price of twice the weight bytes per tap (16 KB slices through a 6-slot ring fed 4 taps ahead).
+// Roles as in halo8: waves 0..7 stream the weight slices (2 KB = 32 rows each), waves 8..15 the halo
+// pieces (4 each: 25 pieces plus duplicates) and the GroupNorm table; all 16 waves transform.
+// ============================================================================================
+namespace halo256 {
+constexpr int TR = 4, TC = 64;
+constexpr int HR = TR + 2, HC = TC + 2;            // 6 x 66 halo pixels
+constexpr int HPIX = HR * HC;                      // 396
+constexpr int NPIECE = (HPIX * 4 + 63) / 64;       // 25 pieces of 1 KB
+constexpr int HBYTES = NPIECE * 1024;              // 25,600
+constexpr int BN = 256, NW = 16, NT = NW * 64;
+constexpr int BBYTES = BN * 64;                    // one tap's 32-channel weight slice: 16 KB
+constexpr int NB = 6, LEAD = 4;                    // weight ring: slices u + 4 (and u + 5) issued at even tap u
+constexpr int PPW = 4;                             // halo pieces per halo wave (8 waves x 4 >= 25)
+constexpr int AB_MAX = 512;
+constexpr int RING = 2 * HBYTES;                   // 51,200
+constexpr int TABLE = RING + NB * BBYTES;          // 149,504
+constexpr int LDS = TABLE + AB_MAX * 8;            // 153,600
+static_assert(LDS <= 160 * 1024, "one block per CU");
+static_assert(NB >= LEAD + 2, "slot of u + LEAD + 1 was last read at tap u - 1 (one barrier per two taps)");
+// epilogue: four passes of 64 tile rows (one 16-row fragment per wave row) x 256 channels: a parked pass
+// (64 x 260 fp32) and two 32 KB residual buffers; pass 0's residual is DMA'd at the last tap into two ring
+// slots the last taps do not read (r0), the other two regions are placed around it
+constexpr int SDW = BN + 4;
+constexpr int PK = 64 * SDW * 4;                   // 66,560
+constexpr int RB = 64 * BN * 2;                    // 32,768
+static_assert(RB == 2 * BBYTES, "pass-0 residual = two ring slots");
+__device__ __forceinline__ int sw(int s) { return ((s >> 2) & 1) << 1; }
+// the first of two adjacent ring slots free at the last tap (slot s = (U - 1) % NB is being read; the
+// barrier of that tap released every slot read before it)
+__host__ __device__ constexpr int r0_slot(int s) { return s <= NB - 3 ? s + 1 : 0; }
+__host__ __device__ constexpr bool plan_ok(int s) {  // park / r0 / r1 disjoint and inside the LDS
+  const int r0 = RING + r0_slot(s) * BBYTES;
+  const int park = r0 >= PK ? 0 : r0 + RB;
+  const int r1 = park == 0 ? (r0 >= PK + RB ? PK : r0 + RB) : 0;
+  auto dis = [](int a, int la, int b, int lb) { return a + la <= b || b + lb <= a; };
+  return r0 + RB <= LDS && park + PK <= LDS && r1 + RB <= LDS && dis(r0, RB, park, PK) && dis(r0, RB, r1, RB) &&
+         dis(park, PK, r1, RB) && dis(r0, RB, RING + s * BBYTES, BBYTES);
+}
+static_assert(plan_ok(0) && plan_ok(1) && plan_ok(2) && plan_ok(3) && plan_ok(4) && plan_ok(5), "epilogue plan");
+}  // namespace halo256
+
+// Epilogue of the 256-channel halo conv (halo_epilogue's arithmetic and statistics order for a 256-wide
+// tile: out = (acc + bias) + residual, bf16; fused GroupNorm partials per (64-row block, channel) as
+// ((g0 + g1) + g2) + g3 of column scans in row order). park / r0 / r1: LDS offsets of the parked pass and
+// the residual buffers of even / odd passes; pass 0's residual is already in flight into r0.
+__device__ __forceinline__ void halo256_res_dma(__amdgpu_buffer_rsrc_t rsr, char* dst, int base, int W, int res_ld,
+                                                int n0, int wave, int lane, int p) {
+  // pass rows: 64 (wave row pr / 16, pixel p * 16 + pr % 16) x 512 B; piece q (this wave's wave and
+  // wave + 16) = rows 2q, 2q + 1; lane i: row 2q + i / 32, chunk i % 32
+  int l = lane;
+  asm volatile("" : "+v"(l));
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = wave + 16 * k;
+    const int pr = 2 * q + (l >> 5);
+    const unsigned vo = (unsigned)(base + (pr >> 4) * W + (pr & 15)) * (unsigned)(res_ld * 2) + (unsigned)((l & 31) * 16);
+    dma16(rsr, dst + q * 1024, vo, p * 16 * res_ld * 2 + n0 * 2);
+  }
+}
+
+__device__ __forceinline__ void halo256_epilogue(const f32x4 (&acc)[4][4], const ConvArgs& a, int n0, int wm, int wn,
+                                                 int tid, char* lds, int base, int W, int park, int r0, int r1,
+                                                 __amdgpu_buffer_rsrc_t rsr, int wave) {
+  using halo256::SDW;
+  asm volatile("" : "+v"(tid));  // addresses derived after the main loop (not hoisted into its live set)
+  const int lane = tid & 63;
+  const int lr = lane & 15, lq = lane >> 4;
+  float* const L = reinterpret_cast<float*>(lds + park);
+  const bool has_res = a.res != nullptr;
+  const bool st = a.gn_part != nullptr;
+  const int cc = tid & 31;  // this thread's 8 channels n0 + 8 cc in every chunk
+  const int nn = n0 + cc * 8;
+  float bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+  if (a.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(a.bias + nn), b1 = *reinterpret_cast<const float4*>(a.bias + nn + 4);
+    bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w; bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+  }
+  float sg[4], qg[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    __syncthreads();  // p = 0: the main loop's LDS reads are done; else: the previous pass's readers are
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) L[(wm * 16 + lq * 4 + r) * SDW + wn * 64 + j * 16 + lr] = acc[p][j][r];
+    if (has_res) {  // this wave's residual pieces of pass p (younger: the 2 stores of pass p - 1)
+      if (p == 0) wait_vm<0>(); else wait_vm<2>();
+    }
+    __syncthreads();
+    if (has_res && p + 1 < 4)  // the next pass's residual into the buffer pass p - 1 read
+      halo256_res_dma(rsr, lds + ((p + 1) & 1 ? r1 : r0), base, W, a.res_ld, n0, wave, lane, p + 1);
+    const char* R = lds + (p & 1 ? r1 : r0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pr = (tid >> 5) + 32 * k;  // pass row: wave row pr / 16, pixel p * 16 + pr % 16 of it
+      const long m = base + (pr >> 4) * W + p * 16 + (pr & 15);
+      const float4 x0 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8 + 4);
+      float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias[e];
+      if (has_res) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + pr * 512 + cc * 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+      }
+      bf16x8 ov;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.out) + m * a.out_ld + nn) = ov;
+      if (st) {
+        *reinterpret_cast<float4*>(L + pr * SDW + cc * 8) = make_float4((float)ov[0], (float)ov[1], (float)ov[2], (float)ov[3]);
+        *reinterpret_cast<float4*>(L + pr * SDW + cc * 8 + 4) = make_float4((float)ov[4], (float)ov[5], (float)ov[6], (float)ov[7]);
+      }
+    }
+    if (st) {  // column scan: thread (wave row b, channel j), the 16 rows of group p, in row order
+      __syncthreads();
+      const int b = tid >> 8, j = tid & 255;
+      const float* col = L + (b * 16) * SDW + j;
+      float y[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) y[r] = col[r * SDW];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s1 += y[r]; s2 = fmaf(y[r], y[r], s2); }
+      sg[p] = s1;
+      qg[p] = s2;
+    }
+  }
+  if (st) {
+    const int b = tid >> 8, j = tid & 255;
+    float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + base + b * W) / 64) * a.cout + n0 + j) * 2;
+    pp[0] = ((sg[0] + sg[1]) + sg[2]) + sg[3];
+    pp[1] = ((qg[0] + qg[1]) + qg[2]) + qg[3];
+    if (tid == 0 && base == 0 && n0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
+  }
+}
+
+template <int GN>
+__global__ __launch_bounds__(1024) void conv3x3_halo256_kernel(ConvArgs a, int tiles_x, int tiles_y, unsigned bytes0,
+                                                              unsigned bytesw) {
+  using namespace halo256;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const hbuf = lds;
+  char* const bbuf = lds + RING;
+  float* const abl = reinterpret_cast<float*>(lds + TABLE);
+  HALO_STAMP(0);
+#ifdef RDEIC_HALO_STAMPS
+  if (threadIdx.x == 0) {
+    g_halo_stamps[(long)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    g_halo_stamps[(long)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
+#endif
+  const int tn = a.cout / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;  // XCD-aware bijective remap (as conv3x3_halo_kernel)
+  const int xcd = orig & 7, q8 = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (orig >> 3);
+  const int nt = wgid % tn;
+  int sp = wgid / tn;
+  const int tx = sp % tiles_x;
+  sp /= tiles_x;
+  const int ty = sp % tiles_y, img = sp / tiles_y;
+  const int oy0 = ty * TR, ox0 = tx * TC, n0 = nt * BN;
+  const int H = a.h, W = a.w, cin = a.c0;
+  const int ncb = cin >> 5, U = ncb * 9;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // wave = (output row, 64-channel quarter)
+  const bool wload = wave < 8;              // weight-stream wave; else halo-stream wave
+  const int hw = wave - 8;
+
+  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)bytes0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)a.weight, (short)0, (int)bytesw, 0x00020000);
+  const bool res_dma = a.res != nullptr;
+  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(res_dma ? a.res : a.in0), (short)0, res_dma ? (int)((long)(img * H + H) * W * a.res_ld * 2) : 0, 0x00020000);
+  // epilogue LDS plan: r0 = two ring slots free at the last tap; the parked pass and r1 around it
+  const int r0 = RING + r0_slot((U - 1) % NB) * BBYTES;
+  const int park = r0 >= PK ? 0 : r0 + RB;  // below r0 when it fits (r0 at ring slot >= 1), else right after it
+  const int r1 = park == 0 ? (r0 >= PK + RB ? PK : r0 + RB) : 0;
+
+  // halo waves: pieces hw + 8 k (k < 4; past the 25 pieces, piece hw + 16 again: same bytes, same slots);
+  // offsets recomputed at each issue from a laundered lane id
+  auto hpiece = [&](int k) { return hw + 8 * k < NPIECE ? hw + 8 * k : hw + 16; };  // wave-uniform
+  auto halo_voff = [&](int k, int ln) {
+    const int p = hpiece(k);
+    const int sl = p * 16 + (ln >> 2), ph = ln & 3;
+    unsigned vo = kOOB;
+    if (sl < HPIX) {
+      const int hr = sl / HC, hc = sl - (sl / HC) * HC;
+      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        vo = (unsigned)((img * H + iy) * W + ix) * (unsigned)(a.ld0 * 2) + (unsigned)((ph ^ sw(sl)) * 16);
+    }
+    return vo;
+  };
+  auto issue_halo = [&](int cb, int k0, int k1) {
+    char* dst = hbuf + (cb & 1) * HBYTES;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int k = k0; k < k1; ++k) dma16(rs0, dst + hpiece(k) * 1024, halo_voff(k, ln), cb * 64);
+  };
+  // transform: wave w takes pieces w + 16 k (k < 2, < 25) whoever loaded them; tinfo: per k a valid bit
+  // (a real piece inside the image) and the lane's logical channel chunk (bits 8 + 2k)
+  unsigned tinfo = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = wave + 16 * k;
+    const int sl = p * 16 + (lane >> 2), ph = lane & 3;
+    bool in = false;
+    if (p < NPIECE && sl < HPIX) {
+      const int hr = sl / HC, hc = sl - (sl / HC) * HC;
+      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+      in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    }
+    if (in) tinfo |= 1u << k;
+    tinfo |= (unsigned)(ph ^ sw(sl)) << (8 + 2 * k);
+  }
+  // weight waves: rows n = 32 wave + 16 k + lane / 4 (k = 0, 1), chunk lane % 4 of every tap slice
+  unsigned bvo0 = kOOB, bvo1 = kOOB;
+  if (wload) {
+    const int na = wave * 32 + (lane >> 2), nb = na + 16, ph = lane & 3;
+    bvo0 = (n0 + na < a.cout) ? (unsigned)(n0 + na) * (unsigned)(a.wld * 2) + (unsigned)((ph ^ sw(na)) * 16) : kOOB;
+    bvo1 = (n0 + nb < a.cout) ? (unsigned)(n0 + nb) * (unsigned)(a.wld * 2) + (unsigned)((ph ^ sw(nb)) * 16) : kOOB;
+  }
+  auto issue_b = [&](int u) {
+    const int cb = u / 9, t = u - (u / 9) * 9;
+    char* dst = bbuf + (u % NB) * BBYTES + wave * 2048;
+    dma16(rsw, dst, bvo0, (t * cin + cb * 32) * 2);
+    dma16(rsw, dst + 1024, bvo1, (t * cin + cb * 32) * 2);
+  };
+  auto transform_piece = [&](int cb, int k) {
+    unsigned info = tinfo;
+    int ln = lane;
+    asm volatile("" : "+v"(info), "+v"(ln));
+    if (!(info & (1u << k))) return;
+    char* pc = hbuf + (cb & 1) * HBYTES + ln * 16 + (wave + 16 * k) * 1024;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(pc);
+    const int ch = (info >> (8 + 2 * k)) & 3;
+    const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb * 32 + ch * 8) * 2);
+    const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
+    const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+    const float bv[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = __builtin_fmaf((float)v[e], av[e], bv[e]);
+      if constexpr (GN == 2) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+      o[e] = (bf16)x;
+    }
+    *reinterpret_cast<bf16x8*>(pc) = o;
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: halo waves bring the table (one piece each; waves past its pieces repeat piece 0) and
+  // block 0's halo; weight waves the first LEAD slices
+  if (wload) {
+    const int n0s = U < LEAD ? U : LEAD;
+    for (int u = 0; u < n0s; ++u) issue_b(u);
+  } else {
+    if constexpr (GN != 0) {
+      const int tbytes = cin * 8, tp = hw < (tbytes + 1023) / 1024 ? hw : 0;
+      const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.gn_ab + (long)img * cin * 2), (short)0, tbytes, 0x00020000);
+      dma16(rst, reinterpret_cast<char*>(abl) + tp * 1024, (unsigned)(tp * 1024 + lane * 16), 0);
+    }
+    issue_halo(0, 0, PPW);
+    wait_vm<0>();
+  }
+  if constexpr (GN != 0) {
+    __syncthreads();  // every table piece and every halo piece of block 0 has landed
+#pragma unroll 1
+    for (int k = 0; k < 2; ++k) transform_piece(0, k);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier releases readers
+  }
+
+  HALO_STAMP(1);
+  const int lr = lane & 15, lq = lane >> 4;
+  const int bsw = (lq ^ sw(lr)) * 16;
+  // Schedule (halo8's): one barrier per two taps, every wait and weight DMA issue at even taps; the next
+  // halo issued in two halves at taps 0 and 2, waited for at tap 4 and transformed at taps 4 and 5 after
+  // each tap's MFMAs; pass 0's residual rows DMA'd at the last tap into two free ring slots.
+  for (int cb = 0; cb < ncb; ++cb) {
+    const bool more = cb + 1 < ncb;
+    const char* hb = hbuf + (cb & 1) * HBYTES;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int u = cb * 9 + t;
+      const bool BAR = t % 2 == 0;  // t is unrolled: a compile-time value
+      if (wload && BAR) {  // slices u and (t < 8) u + 1 landed; issued so far: up to u + 3 (2 DMAs each)
+        if (u + LEAD + 1 < U) {
+          t < 8 ? wait_vm<4>() : wait_vm<6>();  // steady state: a compile-time count
+        } else {
+          const int issued = u + LEAD - 1 < U - 1 ? u + LEAD - 1 : U - 1;
+          const int need = (t < 8 && u + 1 < U) ? u + 1 : u;
+          wait_vm_rt(2 * (issued - need));
+        }
+      }
+      if (!wload && more && t == 4) wait_vm<0>();  // this wave's pieces of the next block have landed
+      if (BAR) __builtin_amdgcn_s_barrier();
+      if (wload) {
+        if (BAR) {  // slices u + 4 and (t < 8) u + 5: slots last read at taps u - 2 and u - 1
+          if (u + LEAD < U) issue_b(u + LEAD);
+          if (t < 8 && u + LEAD + 1 < U) issue_b(u + LEAD + 1);
+        }
+      } else if (t == 0 && more) {  // the next halo's pieces in two halves
+        issue_halo(cb + 1, 0, PPW / 2);
+      } else if (t == 2 && more) {
+        issue_halo(cb + 1, PPW / 2, PPW);
+      }
+      if (t == 8 && !more && res_dma)  // pass 0's residual rows into the two ring slots the last taps do not read
+        halo256_res_dma(rsr, lds + r0, (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
+      // per-tap lane addresses from laundered bases (hoisted over the 9 unrolled taps, with the ring slot
+      // not a multiple of 9 taps, hipcc kept 15 of them in scratch and reloaded them in the loop)
+      int bl = (wn * 64 + lr) * 64 + bsw;
+      int lb = wm * HC + lr;
+      asm volatile("" : "+v"(bl), "+v"(lb));
+      const char* bb = bbuf + (u % NB) * BBYTES + bl;
+      const int ky = t / 3, kx = t - (t / 3) * 3;
+      bf16x8 bfv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(bb + j * 16 * 64);
+      const int sl = lb + ky * HC + kx;
+      const char* ab = hb + sl * 64 + ((lq ^ sw(sl)) << 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ab + i * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+      }
+      if constexpr (GN != 0)
+        if (t >= 4 && t < 6 && more) {
+          transform_piece(cb + 1, t - 4);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // written before the next barrier
+        }
+    }
+  }
+  HALO_STAMP(2);
+  halo256_epilogue(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park, r0, r1, rsr, wave);
+  HALO_STAMP(3);
+}
+
+int g_halo256 = 1;  // the 256-channel halo conv where it applies (rdeic_set_conv_option(10, v))
+
 int g_halo8 = 1;  // the 8-row halo conv where it applies (rdeic_set_conv_option(9, v))
 
 int g_halo = 1;  // 3x3 halo conv: 0 off, 1 for GroupNorm-input convs (default), 2 for every eligible conv
@@ -1932,6 +2291,17 @@ int launch_halo(const rdeic_conv_desc* d, ConvArgs a, hipStream_t s, bool* fused
     rdeic_count_launch(RDEIC_COUNT_HALO_CONV);
     const bool fe = !e.out_f32 && !e.emb && e.act == 0;
     const int gm = e.gn_ab ? (e.gn_silu ? 2 : 1) : 0;
+    if (g_halo256 && fe && d->cout % halo256::BN == 0) {  // 4 x 64 pixels x 256 channels, one block per CU
+      rdeic_count_launch(RDEIC_COUNT_HALO256);
+      const int txw = d->w / halo256::TC, tyw = d->h / halo256::TR;
+      const dim3 gw((unsigned)((long)e.n * tyw * txw * (d->cout / halo256::BN))), bw2(halo256::NT);
+      if (gm == 2) hipLaunchKernelGGL((conv3x3_halo256_kernel<2>), gw, bw2, halo256::LDS, s, e, txw, tyw, b0, bw);
+      else if (gm == 1) hipLaunchKernelGGL((conv3x3_halo256_kernel<1>), gw, bw2, halo256::LDS, s, e, txw, tyw, b0, bw);
+      else hipLaunchKernelGGL((conv3x3_halo256_kernel<0>), gw, bw2, halo256::LDS, s, e, txw, tyw, b0, bw);
+      const int rc = launch_status();
+      if (rc != RDEIC_OK) return rc;
+      continue;
+    }
     if (g_halo8 && fe && d->h % halo8::TR == 0) {  // the 8-row, one-block-per-CU form
       const int tx8 = d->w / halo8::TC, ty8 = d->h / halo8::TR;
       const dim3 g8((unsigned)((long)e.n * ty8 * tx8 * (d->cout / halo8::BN))), b8(halo8::NT);
@@ -2213,5 +2583,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 6) { int prev = g_halo; g_halo = value; return prev; }
   if (key == 8) { int prev = rdeic_g_attn512; rdeic_g_attn512 = value; return prev; }
   if (key == 9) { int prev = g_halo8; g_halo8 = value; return prev; }
+  if (key == 10) { int prev = g_halo256; g_halo256 = value; return prev; }
   return RDEIC_EINVAL;
 }
