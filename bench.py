@@ -87,6 +87,8 @@ def parse(argv=None):
     ap.add_argument("--no-geglu-fuse", action="store_true", help="unfused GEGLU (projection + geglu kernel), A/B only")
     ap.add_argument("--no-splitk-entropy", action="store_true", help="no split-K in the bf16 entropy nets, A/B only")
     ap.add_argument("--no-halo", action="store_true", help="materialised GroupNorm + im2col conv, A/B only")
+    ap.add_argument("--conv-option", action="append", default=[], metavar="KEY=VALUE",
+                    help="rdeic_set_conv_option(KEY, VALUE) before the run (include/rdeic_hip.h), A/B only")
     ap.add_argument("--rate-gain", type=float, default=None,
                     help="synthetic bpp knob (rdeic_amd/weights.py); default: the ~0.08 bpp gain of config 2")
     ap.add_argument("--fp32-steps", type=int, default=2,
@@ -152,6 +154,9 @@ def main():
         ops.SPLITK_ENTROPY = False
     if args.no_halo:
         ops.set_halo_conv(0)
+    for kv in args.conv_option:
+        k, v = kv.split("=")
+        ops.set_conv_option(int(k), int(v))
 
     imgs = torch.from_numpy(np.stack([synth_image(S, S, 231 + g) for g in range(g0, g1)])).to(dev)
     draws = [relay_noise((1, 4, S // 8, S // 8), 231 + g, args.ddim_steps) for g in range(g0, g1)]

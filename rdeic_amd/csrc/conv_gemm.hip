@@ -2252,7 +2252,9 @@ __global__ __launch_bounds__(1024) void conv3x3_halo256_kernel(ConvArgs a, int t
   HALO_STAMP(3);
 }
 
-int g_halo256 = 1;  // the 256-channel halo conv where it applies (rdeic_set_conv_option(10, v))
+// the 256-channel halo conv where it applies (rdeic_set_conv_option(10, v)); off by default: measured 2-3%
+// slower than halo8 on every VAE cout >= 256 shape and -0.6% on the bench (profiles/r05_halo256_ab.txt)
+int g_halo256 = 0;
 
 int g_halo8 = 1;  // the 8-row halo conv where it applies (rdeic_set_conv_option(9, v))
 

@@ -43,6 +43,10 @@ from tests.golden.make_golden import fill_module, schedule  # noqa: E402
 from tests.golden.train_proj import projections  # noqa: E402
 
 SIZE = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+# "f64" as the second argument: the same step in float64 (r05, the conditioning of the fp32 gradients):
+# writes train_{SIZE}_f64.npz with the loss terms and every gradient's sum / norm / projections only
+F64 = len(sys.argv) > 2 and sys.argv[2] == "f64"
+DT = torch.float64 if F64 else torch.float32
 SEED = 5
 L_GUIDE, L_BPP, LR = 3.0, 1.0, 2e-5
 FULL_GRADS = ("control_model.control_model.input_blocks.0.0.weight", "control_model.enc_zero_convs_out.0.0.weight",
@@ -67,27 +71,32 @@ def main():
     for m, p in [(unet, "model.diffusion_model."), (ne, "control_model."), (enc, "first_stage_model.encoder."),
                  (quant_conv, "first_stage_model.quant_conv."), (comp, "preprocess_model.")]:
         fill_module(m, p)
+    for m in (unet, ne, enc, quant_conv, comp):
+        m.to(DT)
     for m in (unet, enc, quant_conv):
         m.requires_grad_(False)
     unet.train(), ne.train(), comp.train()
     sched = schedule(R)
     ac = sched["alphas_cumprod"].double().numpy()
-    f32 = lambda a: torch.tensor(a, dtype=torch.float32)  # noqa: E731
+    sched = {k: v.to(DT) for k, v in sched.items()}
+    f32 = lambda a: torch.tensor(a, dtype=DT)  # noqa: E731
     sqrt_recip = f32(np.sqrt(1.0 / ac))
     sqrt_recipm1 = f32(np.sqrt(1.0 / ac - 1))
     lamba = sqrt_recipm1[cfg["used_timesteps"] - 1]
 
     img = synth_image(SIZE, SIZE, 231)
-    ctx = synth_context()
+    ctx = synth_context().to(DT)
     hl = SIZE // 8
     dr = train_draws(1, hl, hl, cfg["compression"]["slice_ch"], SEED, cfg["used_timesteps"])
+    dr = {k: ([s.to(DT) for s in v] if isinstance(v, list) else (v.to(DT) if v.is_floating_point() else v))
+          for k, v in dr.items()}
     t = dr["t"]
     out = {"image": img, "t": t.numpy(), "post_eps": dr["post_eps"].numpy(),
            "noise": dr["noise"].numpy()}
     for i, s in enumerate(dr["slice_noise"]):
         out[f"slice_noise{i}"] = s.numpy()
     t0 = time.time()
-    x = torch.tensor(img[None] / 255.0, dtype=torch.float32).permute(0, 3, 1, 2).contiguous()
+    x = torch.tensor(img[None] / 255.0, dtype=DT).permute(0, 3, 1, 2).contiguous()
     with torch.no_grad():  # LatentDiffusion.get_input / encode_first_stage (ddpm.py:777-789, 857-860)
         h_out, c = enc.forward_hc(x * 2 - 1)
         moments = quant_conv(h_out)
@@ -150,6 +159,11 @@ def main():
     out["grad_sum"] = np.asarray(sums)
     out["grad_norm"] = np.asarray(norms)
     out["grad_proj"] = np.stack(projs)
+    if F64:
+        path = os.path.join(HERE, f"train_{SIZE}_f64.npz")
+        np.savez_compressed(path, **{k: v for k, v in out.items() if k.startswith("loss_") or k.startswith("grad_")})
+        print("wrote", path)
+        return
     # AdamW step (torch.optim.AdamW defaults, lr from the fine-tune config)
     opt = torch.optim.AdamW([p for _, p in params], lr=LR)
     opt.step()
