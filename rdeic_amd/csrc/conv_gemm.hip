@@ -1863,8 +1863,20 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
       } else if (t == 2 && more) {
         issue_halo(cb + 1, PPW / 2, PPW);
       }
-      if (t == 8 && !more && res_dma)  // pass 0's residual rows into the halo buffer the last block does not read
-        halo_res_dma<NW>(rsr, lds + res_off(f, 0), (img * H + oy0) * W + ox0, W, a.res_ld, n0, wave, lane, 0);
+      // pass 0's residual rows (32 KB) into the halo buffer the last channel block does not read, issued by the
+      // halo waves at the last block's tap 0 (they load nothing else in it): nine taps of lead for the HBM
+      // latency the epilogue's first pass used to wait on (issued at tap 8: +8.6k cycles per block, r05 stamps)
+      if (t == 0 && !more && res_dma && !wload) {
+        int l = lane;
+        asm volatile("" : "+v"(l));
+        const int base = (img * H + oy0) * W + ox0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = hw + 8 * k, pr = 4 * q + (l >> 4);
+          const unsigned vo = (unsigned)(base + (pr >> 4) * W + (pr & 15)) * (unsigned)(a.res_ld * 2) + (unsigned)((l & 15) * 16);
+          dma16(rsr, lds + res_off(f, 0) + q * 1024, vo, n0 * 2);
+        }
+      }
       const char* bb = bbuf + (u % NB) * BBYTES + (wn * 64 + lr) * 64 + bsw;
       const int ky = t / 3, kx = t - (t / 3) * 3;
       bf16x8 bfv[4];

@@ -73,6 +73,31 @@ def main():
         fill_module(m, p)
     for m in (unet, ne, enc, quant_conv, comp):
         m.to(DT)
+    if F64:  # the reference casts to the UNets' `dtype` attribute and builds the timestep embedding in fp32
+        for m in (unet, ne):
+            for sub in m.modules():
+                if isinstance(getattr(sub, "dtype", None), torch.dtype) and "dtype" in vars(sub):
+                    sub.dtype = DT
+        for mod in list(sys.modules.values()):
+            f = getattr(mod, "timestep_embedding", None) if mod is not None else None
+            if callable(f) and not getattr(f, "_f64", False):
+                def emb64(*a, _f=f, **k):
+                    return _f(*a, **k).to(DT)
+                emb64._f64 = True
+                setattr(mod, "timestep_embedding", emb64)
+        import types
+        for mod in list(sys.modules.values()):  # the CrossAttention fp32 upcast of q, k: skipped in f64
+            if mod is not None and getattr(mod, "_ATTN_PRECISION", None) == "fp32":
+                mod._ATTN_PRECISION = "f64"
+        for m in (unet, ne, comp):  # GroupNorm32.forward upcasts to fp32 (x.float()): the plain GroupNorm instead
+            for sub in m.modules():
+                if isinstance(sub, torch.nn.GroupNorm) and type(sub) is not torch.nn.GroupNorm:
+                    sub.forward = types.MethodType(torch.nn.GroupNorm.forward, sub)
+        for obj in (ne,):  # NoiseEstimator's globals (AST-extracted module dict)
+            g = type(obj).forward.__globals__
+            f = g.get("timestep_embedding")
+            if callable(f) and not getattr(f, "_f64", False):
+                g["timestep_embedding"] = lambda *a, _f=f, **k: _f(*a, **k).to(DT)
     for m in (unet, enc, quant_conv):
         m.requires_grad_(False)
     unet.train(), ne.train(), comp.train()
@@ -105,6 +130,8 @@ def main():
         std = torch.exp(0.5 * logvar)
         x_start = cfg["scale_factor"] * (mean + std * dr["post_eps"])
         h = cfg["scale_factor"] * c
+    if F64:  # tensors the reference creates inside its forward (VQ one-hot encodings) follow the default dtype
+        torch.set_default_dtype(torch.float64)
     train_ref.NOISE_QUEUE[:] = list(dr["slice_noise"])
     c_latent, lik, qlik, emb_loss, guide_hint = comp(h)
     assert not train_ref.NOISE_QUEUE
