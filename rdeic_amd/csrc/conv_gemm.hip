@@ -136,7 +136,7 @@ struct RowsFrom {
   __device__ __forceinline__ int operator()(int r) const { return m0 + r; }
 };
 
-template <int BM, int BN, int WGM, int WGN, int NT, int P = 2, class RowMap = RowsFrom>
+template <int BM, int BN, int WGM, int WGN, int NT, int P = 2, class RowMap = RowsFrom, bool PF = true>
 __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16], const ConvArgs& a,
                                              int m0, int n0, int wm, int wn, int lane, int tid, char* lds,
                                              RowMap rmap = RowMap{0}) {
@@ -168,9 +168,50 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
   for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int g = 0; g < 4; ++g) sg[u][g] = qg[u][g] = 0.f;
+  // The per-chunk global operands (residual rows, LayerNorm row statistics, bias, LayerNorm column sums)
+  // are loaded at the top of each pass, before the accumulators are parked, behind raw barriers (no
+  // vmcnt(0) drain): their latency overlaps the park instead of being exposed once per chunk in a chain
+  // (r05: the loads inside the chunk loop made the epilogue 19.5k cycles of a 38k-cycle 256x256 linear tile,
+  // tools/dma_stamps.hip). Loaded values and the arithmetic order are unchanged: outputs are bit-identical.
+  constexpr int NCH = (PR * CPR + NT - 1) / NT;  // chunks per thread per pass
+  constexpr int NPF = !PF ? 0 : NCH < 2 ? NCH : 2;  // of them prefetched (register budget; PF off: none)
+  constexpr bool HOIST = PF && (NT % CPR) == 0;   // every chunk of a thread has the same 8 channels
+  auto bar = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  float4 bh[2] = {float4{0.f, 0.f, 0.f, 0.f}, float4{0.f, 0.f, 0.f, 0.f}}, chh[2] = {bh[0], bh[0]};
+  if constexpr (HOIST) {  // bias / LayerNorm column sums of this thread's channels, once
+    const int nn = n0 + (tid % CPR) * 8;
+    if (nn < a.cout) {
+      if (a.bias) {
+        bh[0] = *reinterpret_cast<const float4*>(a.bias + nn);
+        bh[1] = *reinterpret_cast<const float4*>(a.bias + nn + 4);
+      }
+      if (a.ln_rows) {
+        chh[0] = *reinterpret_cast<const float4*>(a.ln_cs + nn);
+        chh[1] = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4);
+      }
+    }
+  }
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    __syncthreads();
+    uint4 rpf[NPF > 0 ? NPF : 1];    // bf16 residual chunk
+    float2 lpf[NPF > 0 ? NPF : 1];   // LayerNorm (mean, rstd) of the chunk's row
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int c = tid + k * NT;
+      const int pr = c / CPR, cc = c - pr * CPR;
+      const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
+      const int m = rmap(wmr * WTM + p * (WTM / P) + wr);
+      const int nn = n0 + cc * 8;
+      const bool ok = c < PR * CPR && m < a.M && nn < a.cout;
+      rpf[k] = uint4{0u, 0u, 0u, 0u};
+      lpf[k] = float2{0.f, 0.f};
+      if (ok) {
+        if (a.res && !of32 && a.out_mode != 2)
+          rpf[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.res) + (long)m * a.res_ld + nn);
+        if (a.ln_rows) lpf[k] = reinterpret_cast<const float2*>(a.ln_rows)[m];
+      }
+    }
+    bar();  // the previous pass's LDS readers are done
 #pragma unroll
     for (int ii = 0; ii < HM; ++ii)
 #pragma unroll
@@ -179,8 +220,11 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
 #pragma unroll
         for (int j = 0; j < TN; ++j) L[pr * SDW + wn * WTN + j * 16 + lr] = acc[p * HM + ii][j][r];
       }
-    __syncthreads();
-    for (int c = tid; c < PR * CPR; c += NT) {
+    bar();
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = tid + k * NT;
+      if (c >= PR * CPR) continue;
       const int pr = c / CPR, cc = c - pr * CPR;
       // pass-local row pr -> wave row block wm' = pr / (WTM/P), row within = pr % (WTM/P)
       const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
@@ -192,16 +236,25 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
       const float4 x1 = *reinterpret_cast<const float4*>(L + pr * SDW + cc * 8 + 4);
       v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
       if (a.ln_rows) {
-        const float2 ms = reinterpret_cast<const float2*>(a.ln_rows)[m];
-        const float4 c0 = *reinterpret_cast<const float4*>(a.ln_cs + nn);
-        const float4 c1 = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4);
+        const float2 ms = k < NPF ? lpf[k < NPF ? k : 0] : reinterpret_cast<const float2*>(a.ln_rows)[m];
+        float4 c0 = chh[0], c1 = chh[1];
+        if constexpr (!HOIST) {
+          c0 = *reinterpret_cast<const float4*>(a.ln_cs + nn);
+          c1 = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4);
+        }
         const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = ms.y * (v[e] - ms.x * cs[e]);
       }
       if (a.bias) {
+        float4 b0 = bh[0], b1 = bh[1];
+        if constexpr (!HOIST) {
+          b0 = *reinterpret_cast<const float4*>(a.bias + nn);
+          b1 = *reinterpret_cast<const float4*>(a.bias + nn + 4);
+        }
+        const float bs[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += a.bias[nn + e];
+        for (int e = 0; e < 8; ++e) v[e] += bs[e];
       }
       if (a.emb) {
         const float* em = a.emb + (long)(m / hw_o) * a.emb_ld + nn;
@@ -231,7 +284,9 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
           v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w; v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
         } else {
           bf16 rv[8];
-          *reinterpret_cast<uint4*>(rv) = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.res) + (long)m * a.res_ld + nn);
+          *reinterpret_cast<uint4*>(rv) =
+              k < NPF ? rpf[k < NPF ? k : 0]
+                      : *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.res) + (long)m * a.res_ld + nn);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += to_f32(rv[e]);
         }
@@ -259,7 +314,7 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
     }
     if constexpr ((WTM == 32 || WTM == 64) && (WTM / P) % 16 == 0) {
       if (st) {
-        __syncthreads();
+        bar();  // LDS-only: the stored values written back (the global stores stay in flight)
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
         const int b = (tid + u * NT) / BN, j = (tid + u * NT) % BN;
@@ -565,7 +620,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_kernel(ConvArgs a) {
 #undef BS
   if constexpr (sizeof(T) == 2 && TM % 2 == 0 && (BM / 2) * (BN + 4) * 4 <= conv_lds_bytes<T, BM, BN, SWZ>()) {
     if (a.epi_vec && epi_vec_ok(a)) {
-      epilogue_vec<BM, BN, WGM, WGN, NT>(acc, a, m0, n0, wm, wn, lane, tid, lds);
+      epilogue_vec<BM, BN, WGM, WGN, NT, 2, RowsFrom, false>(acc, a, m0, n0, wm, wn, lane, tid, lds);
       return;
     }
   }
@@ -908,6 +963,18 @@ __device__ __forceinline__ void epilogue_scalar(const f32x4 (&acc)[TM][TN], cons
   }
 }
 
+#ifdef RDEIC_HALO_STAMPS
+// diagnostic build only (tools/halo_stamps.hip, tools/dma_stamps.hip): per-block shader-clock stamps, 8 u64 per block,
+// written by thread 0 with ordinary vector stores into a buffer nothing else reads
+__device__ unsigned long long* g_halo_stamps;
+#define HALO_STAMP(k)                                                                      \
+  do {                                                                                     \
+    if (threadIdx.x == 0) g_halo_stamps[(long)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define HALO_STAMP(k) do {} while (0)
+#endif
+
 template <int BM, int BN, int WGM, int WGN, int S, int EP>
 __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1,
                                               unsigned bytesw) {
@@ -922,6 +989,7 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
   static_assert(S >= 2 && S <= 4 && PER * (S - 2) <= 63, "ring");
 
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  HALO_STAMP(0);
 
   int kt_begin = 0, kt_end = a.nk;
   if (a.splits > 1) {  // split-K: blockIdx.z = k-range, raw fp32 partial sums into slab z
@@ -1039,6 +1107,7 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(kt_begin + s, s);
+  HALO_STAMP(1);
 
   for (int t = 0; t < nk; ++t) {
     if constexpr (S == 2) {
@@ -1068,13 +1137,16 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
     }
   }
 
+  HALO_STAMP(2);
   if constexpr (TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * STAGE) {
     if ((a.epi_vec || a.out_mode == 2) && epi_vec_ok(a)) {
       epilogue_vec<BM, BN, WGM, WGN, NT, EP>(acc, a, m0, n0, wm, wn, lane, tid, lds);
+      HALO_STAMP(3);
       return;
     }
   }
   epilogue_scalar<TM, TN, WTM, WTN>(acc, a, m0, n0, wm, wn, lane);
+  HALO_STAMP(3);
 }
 
 // Kernel entry points. Residency: 1024-thread blocks need <= 80 SGPRs for two blocks per CU (the
@@ -1414,17 +1486,6 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
   }
 }
 
-#ifdef RDEIC_HALO_STAMPS
-// diagnostic build only (tools/halo_stamps.hip): per-block shader-clock stamps, 8 u64 per block,
-// written by thread 0 with ordinary vector stores into a buffer nothing else reads
-__device__ unsigned long long* g_halo_stamps;
-#define HALO_STAMP(k)                                                                      \
-  do {                                                                                     \
-    if (threadIdx.x == 0) g_halo_stamps[(long)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define HALO_STAMP(k) do {} while (0)
-#endif
 // GN: 0 plain conv, 1 GroupNorm affine on the input, 2 affine + SiLU (compile-time: no per-element branch);
 // FE: the fast epilogue (halo_epilogue: bf16 out, no emb / activation), else epilogue_vec
 template <int GN, bool FE>
@@ -1628,8 +1689,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     halo_epilogue<NW>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(parity),
                       res_off(parity, 0), res_off(parity, 1), rsr, wave);
   else
-    epilogue_vec<TR * TC, BN, 4, 2, NT, 2>(acc, a, 0, n0, wm, wn, lane, tid, lds,
-                                           Rows{(img * H + oy0) * W + ox0, W});
+    epilogue_vec<TR * TC, BN, 4, 2, NT, 2, Rows, false>(acc, a, 0, n0, wm, wn, lane, tid, lds,
+                                                        Rows{(img * H + oy0) * W + ox0, W});
   HALO_STAMP(3);
 }
 

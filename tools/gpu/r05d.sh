@@ -11,3 +11,9 @@ for l in open('$O/stamps.jsonl'):
     d=json.loads(l); c=d['cycles']
     print(d['shape'], 'res',d['res'], 'ms',d['ms'],'TF',d['tflops'],'pro',c['prologue_med'],'main',c['main_med'],'epi',c['epilogue_med'],'blk',c['block_med'])
 "
+for sh in "65536 320 2560 32 1 0" "65536 320 2560 34 1 0" "65536 320 960 32 0 0" "65536 320 320 34 0 1" "65536 1280 320 37 0 1" "16384 640 5120 32 1 0" "4096 1280 10240 32 1 0" "65536 320 2560 32 0 0"; do
+  timeout -k 5 60 tools/dma_stamps $sh >> $O/dma_stamps.jsonl 2>> $O/err.txt || { echo "dma stamps failed"; tail $O/err.txt; exit 5; }
+done
+cat $O/dma_stamps.jsonl
+timeout -k 10 400 python3 -u tools/grad_dump.py $O > $O/grad_dump.log 2>&1 || { echo "grad dump failed"; tail $O/grad_dump.log; exit 6; }
+tail -2 $O/grad_dump.log
