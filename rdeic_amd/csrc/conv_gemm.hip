@@ -47,6 +47,8 @@ struct ConvArgs {
   int gn_hw;                 // pixels per image of the GroupNorm those statistics feed
   const float* ln_rows;      // folded LayerNorm: [M][2] (mean, rstd) of the raw input rows, or NULL
   const float* ln_cs;        // ... and the column sums of the packed (gamma-scaled) bf16 weight
+  float* sk_ws;              // split-K folded into the producer (LDS-DMA path): raw fp32 partial slabs ...
+  int* sk_cnt;               // ... and one arrival counter per output tile (zero before, left zero after)
 };
 
 // Folded LayerNorm (rdeic_conv_desc.ln_rows): LN(x) W = rstd (x W' - mean colsum(W')) with W' = diag(gamma) W
@@ -839,13 +841,11 @@ int launch_smallc(const ConvArgs& a, hipStream_t s) {
   return launch_status();
 }
 
-// Deterministic split-K reduction + epilogue: out = act(sum_z part[z] + bias + emb) + res, the
-// splits summed in index order in fp32 (8 channels per thread, 16-byte loads / stores).
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, const float* __restrict__ part) {
-  const int cp = a.cout >> 3;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)a.M * cp) return;
-  const int m = (int)(i / cp), nn = (int)(i - (long)m * cp) * 8;
+// Deterministic split-K reduction + epilogue of one 8-channel chunk: out = act(sum_z part[z] + bias + emb)
+// + res, the splits summed in index order in fp32 (16-byte loads / stores); st (optional) receives the
+// stored values as fp32 (the fused GroupNorm statistics of the split-K fold).
+__device__ __forceinline__ void splitk_reduce_chunk(const ConvArgs& a, const float* __restrict__ part, int m, int nn,
+                                                    float* st = nullptr) {
   const long slab = (long)a.M * a.cout;
   float v[8];
   {
@@ -872,12 +872,86 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, const fl
     float* o = reinterpret_cast<float*>(a.out) + (long)m * a.out_ld + nn;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = v[e];
+    if (st) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st[e] = v[e];
+    }
   } else {
     bf16 ov[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) ov[e] = from_f32<bf16>(v[e]);
     *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + nn) = *reinterpret_cast<uint4*>(ov);
+    if (st) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st[e] = to_f32(ov[e]);
+    }
   }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, const float* __restrict__ part) {
+  const int cp = a.cout >> 3;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)a.M * cp) return;
+  const int m = (int)(i / cp), nn = (int)(i - (long)m * cp) * 8;
+  splitk_reduce_chunk(a, part, m, nn);
+}
+
+// The split-K reduction folded into the producer (stream-K "fixup"): every split block of an output tile
+// writes its raw fp32 partial slab, then counts itself in; the LAST block to arrive sums the tile's slabs in
+// split order (splitk_reduce_chunk: the same arithmetic as the reduce kernel, so outputs are bit-identical)
+// and, when the output feeds a GroupNorm, writes its canonical statistics (per channel and 64-row block,
+// four 16-row groups summed sequentially, ((g0 + g1) + g2) + g3: gn_rows_partial_kernel's order). No
+// separate reduce / statistics launches. lds: >= BM / 16 * BN * 8 bytes, free.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void splitk_fold(const ConvArgs& a, int tile, int m0, int n0, int tid, char* lds) {
+  __threadfence();  // this block's partial slab is visible device-wide before it counts itself in
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(lds);
+  if (tid == 0) *flag = atomicAdd(a.sk_cnt + tile, 1) == a.splits - 1;
+  __syncthreads();
+  if (!*flag) return;
+  __threadfence();  // acquire: the other splits' slabs
+  constexpr int CPR = BN / 8, G = BM / 16;
+  if (!a.gn_part) {
+    for (int c = tid; c < BM * CPR; c += NT) {
+      const int m = m0 + c / CPR, nn = n0 + (c % CPR) * 8;
+      if (m < a.M && nn < a.cout) splitk_reduce_chunk(a, a.sk_ws, m, nn);
+    }
+  } else {
+    __syncthreads();  // every thread has read the flag before the statistics reuse the LDS
+    float* red = reinterpret_cast<float*>(lds);  // [G][BN][2]
+    for (int w = tid; w < G * CPR; w += NT) {
+      const int g = w / CPR, cc = w % CPR, nn = n0 + cc * 8;
+      float s1[8], s2[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 16 * g + r;
+        if (m < a.M && nn < a.cout) {
+          float y[8];
+          splitk_reduce_chunk(a, a.sk_ws, m, nn, y);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[e] += y[e]; s2[e] = fmaf(y[e], y[e], s2[e]); }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(g * BN + cc * 8 + e) * 2] = s1[e];
+        red[(g * BN + cc * 8 + e) * 2 + 1] = s2[e];
+      }
+    }
+    __syncthreads();
+    for (int w = tid; w < (BM / 64) * BN; w += NT) {
+      const int b = w / BN, j = w % BN, nn = n0 + j;
+      if (m0 + 64 * b >= a.M || nn >= a.cout) continue;
+      const float* q = red + ((4 * b) * BN + j) * 2;
+      float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0 + 64 * b) / 64) * a.cout + nn) * 2;
+      pp[0] = ((q[0] + q[2 * BN]) + q[4 * BN]) + q[6 * BN];
+      pp[1] = ((q[1] + q[2 * BN + 1]) + q[4 * BN + 1]) + q[6 * BN + 1];
+    }
+    if (tid == 0 && m0 == 0 && n0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
+  }
+  if (tid == 0) a.sk_cnt[tile] = 0;  // every split has arrived: reset for the next launch
 }
 
 
@@ -903,6 +977,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(ConvArgs a, const fl
 // conv_kernel), so results are bit-identical to every other bf16 path.
 // ============================================================================================
 constexpr unsigned kOOB = 0x80000000u;  // voffset that reads zeros (buffers are < 2 GiB)
+// split-K workspace layout (rdeic_conv2d_splitk): SK_CNT int32 tile counters (zero, left zero), then the
+// fp32 partial slabs
+constexpr int SK_CNT = 4096;
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -996,7 +1073,7 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
     const int z = blockIdx.z;
     kt_begin = min(a.nk, z * a.kper);
     kt_end = min(a.nk, kt_begin + a.kper);
-    a.out += (long)z * a.M * a.out_ld * 4;
+    if (!a.sk_cnt) a.out += (long)z * a.M * a.out_ld * 4;  // (the folded form writes a.sk_ws, below)
   } else if (gridDim.z > 1) {
     const long z = blockIdx.z;
     a.in0 += z * a.in_bs * 2; a.in1 += z * a.in_bs * 2;
@@ -1138,6 +1215,25 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
   }
 
   HALO_STAMP(2);
+  // split-K folded into the producer: partial slab, then the last split reduces (the split launches run the
+  // heuristic's 4- and 8-wave tiles, launch_dma_auto(tile -1); compiled only there: register budget)
+  if constexpr (WGM * WGN <= 8) if (a.splits > 1 && a.sk_cnt) {
+    ConvArgs p = a;
+    p.out = reinterpret_cast<char*>(a.sk_ws + (long)blockIdx.z * a.M * a.cout);
+    p.out_ld = a.cout; p.out_f32 = 1; p.out_mode = 0;
+    p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr; p.ln_rows = nullptr;
+    bool done = false;
+    if constexpr (TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * STAGE) {
+      if (p.epi_vec && epi_vec_ok(p)) {
+        epilogue_vec<BM, BN, WGM, WGN, NT, EP>(acc, p, m0, n0, wm, wn, lane, tid, lds);
+        done = true;
+      }
+    }
+    if (!done) epilogue_scalar<TM, TN, WTM, WTN>(acc, p, m0, n0, wm, wn, lane);
+    splitk_fold<BM, BN, NT>(a, wgid, m0, n0, tid, lds);
+    HALO_STAMP(3);
+    return;
+  }
   if constexpr (TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * STAGE) {
     if ((a.epi_vec || a.out_mode == 2) && epi_vec_ok(a)) {
       epilogue_vec<BM, BN, WGM, WGN, NT, EP>(acc, a, m0, n0, wm, wn, lane, tid, lds);
@@ -1197,8 +1293,11 @@ bool dma_vec_epilogue(const ConvArgs& a) {
 template <int BM, int BN, int WGM, int WGN, int S, int EP>
 int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int gn_hw, bool* fused) {
   if (a.gn_part) {
-    const bool ok = a.splits <= 1 && a.batch == 1 && a.out_mode == 0 && gn_hw > 0 && gn_hw % 64 == 0 &&
-                    stats_tile_ok<BM, BN, WGM, WGM * WGN * 64, EP>() && dma_vec_epilogue<BM, BN, WGM, WGN, S, EP>(a);
+    const bool ok = a.splits > 1 && a.sk_cnt  // the split-K fold's last block writes them
+                        ? a.batch == 1 && a.out_mode == 0 && gn_hw > 0 && gn_hw % 64 == 0 && BM % 64 == 0
+                        : a.splits <= 1 && a.batch == 1 && a.out_mode == 0 && gn_hw > 0 && gn_hw % 64 == 0 &&
+                              stats_tile_ok<BM, BN, WGM, WGM * WGN * 64, EP>() &&
+                              dma_vec_epilogue<BM, BN, WGM, WGN, S, EP>(a);
     if (!ok) a.gn_part = nullptr;
     if (fused) *fused = ok;
   }
@@ -1271,11 +1370,13 @@ int dma_grouped(const rdeic_conv_desc* d, int tile, int splits, float* ws, hipSt
   if (make_args(d, a, vec) != RDEIC_OK || !vec) return -1;
   unsigned b0, b1, bw;
   if (dma_ok(d, a, b0, b1, bw)) {
-    if (splits > 1) {
+    if (splits > 1) {  // folded split-K: the real epilogue stays in the arguments, partial slabs after the counters
       a.splits = splits; a.kper = (a.nk + splits - 1) / splits;
-      a.bias = nullptr; a.emb = nullptr; a.act = 0; a.res = nullptr; a.ln_rows = nullptr;
-      a.out = (char*)ws; a.out_ld = a.cout; a.out_f32 = 1; a.out_mode = 0;
-      a.gn_part = nullptr;
+      a.sk_cnt = reinterpret_cast<int*>(ws);
+      a.sk_ws = ws + SK_CNT;
+      // the fold is compiled into the 4- and 8-wave tiles only (conv_dma_body): 128x128 / 8 waves when the
+      // split grid fills the chip, else 64x128 / 4 waves (the heuristic's small-grid choices)
+      tile = (long)cdiv(a.M, 128) * cdiv(a.cout, 128) * splits >= 256 ? 25 : 26;
     }
     return launch_dma_auto(a, b0, b1, bw, s, tile, d->gn_hw, fused);
   }
@@ -2330,6 +2431,7 @@ __global__ __launch_bounds__(1024) void conv3x3_halo256_kernel(ConvArgs a, int t
 int g_halo256 = 0;
 
 int g_halo8 = 1;  // the 8-row halo conv where it applies (rdeic_set_conv_option(9, v))
+int g_sk_fold = 1;  // split-K reduction folded into the producer (rdeic_set_conv_option(11, v))
 
 int g_halo = 1;  // 3x3 halo conv: 0 off, 1 for GroupNorm-input convs (default), 2 for every eligible conv
 
@@ -2407,6 +2509,8 @@ int launch_halo(const rdeic_conv_desc* d, ConvArgs a, hipStream_t s, bool* fused
 namespace {
 // descriptor -> kernel arguments (validation shared by rdeic_conv2d / rdeic_conv2d_splitk)
 int make_args(const rdeic_conv_desc* d, ConvArgs& a, bool& vec) {
+  a.sk_ws = nullptr;
+  a.sk_cnt = nullptr;
   if (!d || !d->in0 || !d->weight || !d->out) return RDEIC_EINVAL;
   if (d->c0 <= 0 || d->c1 < 0 || (d->c1 > 0 && !d->in1) || d->cout <= 0 || d->kh <= 0 || d->kw <= 0 ||
       d->stride <= 0 || d->n <= 0 || d->ho <= 0 || d->wo <= 0)
@@ -2567,7 +2671,7 @@ static int conv2d_impl(const rdeic_conv_desc* d, int32_t tile, void* stream) {
 // out_mode 0, batch 1, cout % 8 == 0. The k-order differs from rdeic_conv2d (not bit-identical
 // to it), so callers that need batch invariance must not use it.
 static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats,
-                              void* stream) {
+                              void* stream, bool* stats_done) {
   ConvArgs a;
   bool vec = false;
   const int rc = make_args(d, a, vec);
@@ -2575,12 +2679,13 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
   if (!vec || d->gn_ab || d->out_mode != 0 || a.batch != 1 || d->cout % 8 || splits < 2 || !ws ||
       (d->out_ld % 8) || ((uintptr_t)d->out % 16) || ((uintptr_t)ws % 16))
     return RDEIC_EINVAL;
-  if (ws_floats < (size_t)splits * a.M * a.cout) return RDEIC_ENOSPC;
+  if (ws_floats < (size_t)SK_CNT + (size_t)splits * a.M * a.cout) return RDEIC_ENOSPC;
   hipStream_t s = (hipStream_t)stream;
+  float* const part = ws + SK_CNT;  // the first SK_CNT words are the folded form's tile counters
   if (d->dtype == 0) {  // fp32: 64x64 register-staged partial tiles, fp32 output from the reduction
     ConvArgs p = a;
     p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr; p.ln_rows = nullptr;
-    p.out = (char*)ws; p.out_ld = a.cout; p.out_f32 = 0;
+    p.out = (char*)part; p.out_ld = a.cout; p.out_f32 = 0;
     p.splits = splits;
     p.kper = (a.nk + splits - 1) / splits;
     dim3 grid(cdiv(a.M, 64), cdiv(a.cout, 64), splits);
@@ -2590,19 +2695,39 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
     a.out_f32 = 1;  // the reduction's output (and residual) type: fp32
     const long chunks = (long)a.M * (a.cout / 8);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, a,
-                       (const float*)ws);
+                       (const float*)part);
     return launch_status();
   }
-  if (g_dma && dma_grouped(d, -1, splits, ws, s) == RDEIC_OK) {
-    a.splits = splits;
-    const long chunks = (long)a.M * (a.cout / 8);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, a,
-                       (const float*)ws);
-    return launch_status();
+  // LDS-DMA path: the reduction (and the output's GroupNorm statistics) folded into the producing launch's
+  // last split per tile (splitk_fold) when the tile counters fit
+  if (g_dma && g_sk_fold && (long)cdiv(a.M, 64) * cdiv(a.cout, 128) <= SK_CNT) {
+    bool fused = false;
+    if (dma_grouped(d, -1, splits, ws, s, &fused) == RDEIC_OK) {
+      if (stats_done) *stats_done = d->gn_part && fused;
+      return launch_status();
+    }
+  }
+  if (g_dma && !g_sk_fold) {  // the unfolded LDS-DMA form (A/B and tests): partial launch, then the reduce kernel
+    rdeic_conv_desc e = *d;
+    e.bias = nullptr; e.emb = nullptr; e.act = 0; e.res = nullptr; e.gn_part = nullptr; e.ln_rows = nullptr;
+    e.out = part; e.out_ld = d->cout; e.out_f32 = 1;
+    ConvArgs pa;
+    bool pv = false;
+    unsigned b0, b1, bw;
+    if (make_args(&e, pa, pv) == RDEIC_OK && pv && dma_ok(&e, pa, b0, b1, bw)) {
+      pa.splits = splits; pa.kper = (pa.nk + splits - 1) / splits;
+      if (launch_dma_auto(pa, b0, b1, bw, s, -1) == RDEIC_OK) {
+        a.splits = splits;
+        const long chunks = (long)a.M * (a.cout / 8);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, a,
+                           (const float*)part);
+        return launch_status();
+      }
+    }
   }
   ConvArgs p = a;  // partial pass: raw sums into the workspace
   p.bias = nullptr; p.emb = nullptr; p.act = 0; p.res = nullptr; p.gn_part = nullptr; p.ln_rows = nullptr;
-  p.out = (char*)ws; p.out_ld = a.cout; p.out_f32 = 1;
+  p.out = (char*)part; p.out_ld = a.cout; p.out_f32 = 1;
   p.splits = splits;
   p.kper = (a.nk + splits - 1) / splits;
   dim3 grid(cdiv(a.M, 128), cdiv(a.cout, 128), splits);
@@ -2611,7 +2736,7 @@ static int conv2d_splitk_impl(const rdeic_conv_desc* d, int32_t splits, float* w
   a.splits = splits;
   const long chunks = (long)a.M * (a.cout / 8);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, a,
-                     (const float*)ws);
+                     (const float*)part);
   return launch_status();
 }
 
@@ -2628,13 +2753,14 @@ extern "C" int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, flo
   if (d && d->gn_part && (d->gn_hw <= 0 || d->gn_hw % 64 || (long)d->n * d->ho * d->wo % d->gn_hw))
     return RDEIC_EINVAL;
   int rc;
+  bool stats_done = false;
   {
     rdeic_prof_add_bytes(conv_bytes(d));
     ProfScope ps((hipStream_t)stream, RDEIC_PROF_CONV, conv_flops(d));
-    rc = conv2d_splitk_impl(d, splits, ws, ws_floats, stream);
+    rc = conv2d_splitk_impl(d, splits, ws, ws_floats, stream, &stats_done);
   }
   if (rc == RDEIC_OK) rdeic_count_launch(RDEIC_COUNT_SPLITK);
-  if (rc != RDEIC_OK || !d->gn_part) return rc;  // statistics of the reduced output: stand-alone pass
+  if (rc != RDEIC_OK || !d->gn_part || stats_done) return rc;  // statistics of the reduced output: stand-alone pass
   return gn_rows_partial(d->out, (long)d->n * d->ho * d->wo, d->cout, d->out_ld, d->gn_hw, d->gn_part,
                          d->out_f32 ? 0 : 1, (hipStream_t)stream);
 }
@@ -2659,5 +2785,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 8) { int prev = rdeic_g_attn512; rdeic_g_attn512 = value; return prev; }
   if (key == 9) { int prev = g_halo8; g_halo8 = value; return prev; }
   if (key == 10) { int prev = g_halo256; g_halo256 = value; return prev; }
+  if (key == 11) { int prev = g_sk_fold; g_sk_fold = value; return prev; }
   return RDEIC_EINVAL;
 }

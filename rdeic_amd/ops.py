@@ -208,7 +208,7 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
 
     tag = ("conv", flops, (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), d.out_mode))
     if splits > 1:
-        ws = _splitk_workspace(splits * n * ho * wo * p.cout, x.device)
+        ws = _splitk_workspace(SPLITK_COUNTERS + splits * n * ho * wo * p.cout, x.device)
         _launch(tag, "rdeic_conv2d_splitk", C.byref(d), splits, ws.data_ptr(), ws.numel(), stream_ptr())
     elif tile >= 0:
         _launch(tag, "rdeic_conv2d_tile", C.byref(d), tile, stream_ptr())
@@ -396,14 +396,20 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
 _SPLITK_KEEP: list = []  # every workspace ever handed out: recorded launch plans hold their pointers
 
 
+# rdeic_conv2d_splitk's workspace starts with this many int32 tile counters (zero; the folded reduction
+# leaves them zero), then the fp32 partial slabs
+SPLITK_COUNTERS = 4096
+
+
 def _splitk_workspace(n: int, device) -> torch.Tensor:
     """Split-K partial-sum scratch, one per (device, stream): concurrent codec sessions (one per
-    stream) must not share it. A grown workspace replaces the old one for new launches, but the
-    old one stays allocated (plans recorded earlier still point at it)."""
+    stream) must not share it (nor its tile counters). A grown workspace replaces the old one for new
+    launches, but the old one stays allocated (plans recorded earlier still point at it)."""
     key = (str(device), stream_ptr())
     buf = _SPLITK_WS.get(key)
     if buf is None or buf.numel() < n:
         buf = torch.empty(n, dtype=torch.float32, device=device)
+        buf[:SPLITK_COUNTERS].zero_()
         _SPLITK_WS[key] = buf
         _SPLITK_KEEP.append(buf)
     return buf

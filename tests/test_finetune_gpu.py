@@ -6,7 +6,8 @@ at 128x128 with the same synthetic weights and seeded draws. The HIP path runs t
 parity mode through the C ABI (forward and backward kernels) and must reproduce:
   * the forward intermediates (x_start, h, c_latent, guide_hint, x_noisy, eps) and every loss term;
   * the gradient of every one of the 663 trainable tensors (76.7M parameters): norm and 4 seeded
-    random projections within 2e-3 of the reference gradient's norm;
+    random projections within TOL_BY_SIZE of the reference gradient's norm, and within TOL64 of the
+    float64 truth (train_{size}_f64.npz: the reference modules run in float64);
   * the VQ codebook re-initialisation (embed_prob, row sums of the updated codebook);
   * the AdamW update (full tensors of a few layers).
 Tolerances are fp32 summation-order bounds (different reduction trees than torch's CPU kernels)."""
@@ -17,10 +18,20 @@ import torch
 pytestmark = pytest.mark.gpu
 
 GOLD = "tests/golden/train_{}.npz"
+GOLD64 = "tests/golden/train_{}_f64.npz"
 TOL = 2e-3
-# fp32 summation-order bound per size: at 512^2 the weight-gradient reductions run over 16x the pixels
-# (measured r04: worst tensor 2.4e-3 of its norm, hyper_dec.0.upsample.0.weight)
-TOL_BY_SIZE = {128: 2e-3, 512: 4e-3}
+# Gradients against the reference's fp32 result: an fp32 summation-order bound. At 512^2 it is not a
+# tight check: the same step run through the reference modules in float64 (make_train_golden.py 512 f64,
+# r05) shows that the reference's OWN fp32 gradients sit up to 1.8e-3 of the norm from the float64 truth
+# on the hyperprior / encoder tensors (the bpp-gradient path; hyper_dec.0.subpel_conv.0.weight 1.8e-3,
+# hyper_dec.0.upsample.0.weight 1.6e-3), so two independent fp32 results differ by up to ~2 x that
+# (measured r04: 2.36e-3 on hyper_dec.0.upsample.0.weight). The 512^2 bar is therefore set against the
+# float64 truth (TOL64), where ours measure 5.7e-5 (128^2) and 1.71e-3 (512^2) at worst (r05,
+# tools/grad_dump.py): >= 3x margin, and our worst may not exceed the reference fp32's own worst by > 1.5x
+# (512^2: 1.71e-3 against 1.81e-3).
+TOL_BY_SIZE = {128: 2e-3, 512: 7.5e-3}  # vs the fp32 golden: two independent fp32 results (worst 2.36e-3)
+TOL64 = {128: 2e-4, 512: 5.5e-3}        # vs the float64 truth (worst 5.7e-5 / 1.71e-3)
+REL_FLOOR = {128: 1e-4, 512: 0.0}       # ours-vs-reference accuracy bar floor (both ~1e-5 at 128^2)
 
 
 # 128^2 (fast) and config 5's own 512^2 (train.py:10-28, configs/finetune_ood.yaml: out_size 512)
@@ -109,6 +120,34 @@ def test_gradients_of_every_trainable_tensor(step):
         if k.startswith("grad:"):
             n = k[5:]
             _close(grads[n].numpy().reshape(g[k].shape), g[k], TOL_BY_SIZE[step["size"]], k)
+
+
+def _err(norm, proj, n64, p64):
+    return max(abs(norm - n64), float(np.abs(proj - p64).max())) / n64
+
+
+def test_gradients_against_float64_truth(step):
+    """Every gradient against the same step computed by the reference's modules in float64: within TOL64 of the
+    norm, and no less accurate overall than the reference's own fp32 gradients (worst error <= 1.5x theirs)."""
+    from tests.golden.train_proj import projections
+    g, grads = step["g"], step["grads"]
+    g64 = np.load(GOLD64.format(step["size"]))
+    names = [str(n) for n in g64["grad_names"]]
+    assert names == [str(n) for n in g["grad_names"]]
+    ours, ref = [], []
+    for i, n in enumerate(names):
+        n64 = float(g64["grad_norm"][i])
+        if n64 == 0.0:
+            continue
+        gr = grads[n]
+        ours.append((_err(float(gr.double().norm()), projections(n, gr), n64, g64["grad_proj"][i]), n))
+        ref.append(_err(float(g["grad_norm"][i]), g["grad_proj"][i], n64, g64["grad_proj"][i]))
+    worst = max(ours)
+    print(f"[{step['size']}] worst gradient error vs float64: ours {worst[0]:.3e} ({worst[1]}), "
+          f"reference fp32 {max(ref):.3e}")
+    bad = [o for o in ours if o[0] > TOL64[step["size"]]]
+    assert not bad, f"{len(bad)} gradients off the float64 truth: {sorted(bad)[-5:]}"
+    assert worst[0] <= 1.5 * max(max(ref), REL_FLOOR[step["size"]]), (worst, max(ref))
 
 
 def test_adamw_update(step):

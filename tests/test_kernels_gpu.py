@@ -414,3 +414,40 @@ def test_layernorm_folded_linear(gpu, rows, cin, couts, geglu):
           f"mean {e_u.mean().item():.3e} (ref max {scale:.2f})")
     assert e_f.max().item() <= 2e-2 * scale
     assert e_f.mean().item() <= 1.5 * e_u.mean().item() + 1e-4  # no worse than the bf16 materialised path
+
+
+@pytest.mark.parametrize("cin,cout,hw,B,act,res,emb,f32", [(1280, 1280, 8, 16, 3, True, True, False),
+                                                         (2560, 1280, 8, 16, 0, False, False, False),
+                                                         (640, 640, 16, 4, 3, True, True, False),
+                                                         (1280, 640, 8, 3, 0, True, False, True)])
+def test_conv_splitk_fold_bit_identical(gpu, cin, cout, hw, B, act, res, emb, f32):
+    """The split-K reduction folded into the producing launch (the last split of each output tile reduces it,
+    rdeic_set_conv_option(11, 1)) against the separate reduce launch (option 11 = 0): the same arithmetic, so
+    outputs and the fused GroupNorm statistics are bit-identical; the tile counters are left zero, so a
+    repeated launch reproduces itself."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(cin + cout + hw + B)
+    x = _nhwc(torch.randn(B, cin, hw, hw, generator=g).to(torch.bfloat16))
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    p = ops.ConvParams.pack(w, torch.randn(cout, generator=g), pad=1, dtype=torch.bfloat16)
+    e = torch.randn(B, cout, generator=g).cuda() if emb else None
+    rd = _nhwc(torch.randn(B, cout, hw, hw, generator=g).to(torch.float32 if f32 else torch.bfloat16)) if res else None
+    gamma, beta = torch.ones(cout, device="cuda"), torch.zeros(cout, device="cuda")
+    outs = []
+    for fold in (1, 1, 0):
+        prev = ops.set_conv_option(11, fold)
+        try:
+            with ops.splitk_allowed():
+                assert ops._splitk_count(x, None, B * hw * hw, p, False, rd if rd is not None else x, B) > 1
+                c0 = ops.launch_count(ops.COUNT_SPLITK)
+                y = ops.conv2d(x, p, emb=e, act=act, res=rd, out_f32=f32, stats=not f32)
+                assert ops.launch_count(ops.COUNT_SPLITK) == c0 + 1
+            ab = None if f32 else ops.group_norm_ab(y, gamma, beta, 32, 1e-5)
+            outs.append((y.clone(), ab))
+        finally:
+            ops.set_conv_option(11, prev)
+    torch.cuda.synchronize()
+    for y, ab in outs[1:]:
+        assert torch.equal(outs[0][0], y)
+        if ab is not None:
+            assert torch.equal(outs[0][1], ab)
