@@ -94,16 +94,17 @@ int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
  * concat segments multiples of 64 channels; other shapes fall back to the register path):
  * 20 256x256/8, 21 256x128/8, 22 128x256/8, 23-24 128x128/4, 25 128x128/8, 26 64x128/4,
  * 27 128x128/8, 28 256x128/8, 29 128x256/8, 30 64x128/4, 31 128x64/4, 32 256x256/16,
- * 33 256x128/16, 34 128x128/16, 35 512x128/16, 36 64x128/8, 37 128x160/4, 38 64x160/4 (ring depths in
- * conv_gemm.hip). -1 = heuristic. All tiles give
+ * 33 256x128/16, 34 128x128/16, 35 512x128/16, 36 64x128/8, 37 128x160/4, 38 64x160/4,
+ * 39 256x128/8 with 32-deep k-tiles (two blocks per CU; ring depths in conv_gemm.hip). -1 = heuristic.
+ * All tiles give
  * bit-identical results (same k order, same MFMA), so a caller may autotune. */
 int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream);
 /* Split-K variant for small-M / large-K layers (the UNet's 8x8 and 16x16 levels): `splits`
  * k-ranges accumulate into the caller's workspace, then a reduction sums them in split order
  * (deterministic) and applies bias / emb / act / residual. ws: 4096 int32 tile counters that must be
- * zero (they are left zero), then >= splits * n*ho*wo * cout fp32 partials (ws_floats counts both). On
- * the LDS-DMA path the reduction, and the output's GroupNorm statistics (gn_part), run in the producing
- * launch: the last split of each output tile reduces it (no reduce / statistics launches).
+ * zero (they are left zero), then >= splits * n*ho*wo * cout fp32 partials (ws_floats counts both). With
+ * rdeic_set_conv_option(11, 1) the LDS-DMA path folds the reduction, and the output's GroupNorm
+ * statistics (gn_part), into the producing launch (the last split of each output tile reduces it).
  * bf16 only, no GN prologue, out_mode 0, batch 1, cout % 8 == 0. Not bit-identical to
  * rdeic_conv2d (different k grouping): not for the entropy-model nets. */
 int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats, void* stream);
@@ -130,8 +131,8 @@ int rdeic_set_conv_path(int32_t path);
  * key 10: the halo conv's 256-channel form (4 x 64 pixels x 256 channels per 1024-thread block) where
  *        cout % 256 == 0 and the epilogue is bf16 without emb / activation: 1 on, 0 off (default: it
  *        measured 2-3% slower than the 8-row form); bit-identical outputs either way;
- * key 11: split-K reduction (and GroupNorm statistics) folded into the producing launch (1, default) /
- *        a separate reduce (and statistics) launch (0); bit-identical outputs and statistics;
+ * key 11: split-K reduction (and GroupNorm statistics) folded into the producing launch (1) / a separate
+ *        reduce (and statistics) launch (0, default: the fold measured slower); bit-identical either way;
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way
  * (keys 0-5; 6 and 8 change fp32 rounding only). */
 int rdeic_set_conv_option(int32_t key, int32_t value);

@@ -1052,27 +1052,37 @@ __device__ unsigned long long* g_halo_stamps;
 #define HALO_STAMP(k) do {} while (0)
 #endif
 
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+// KB: k per LDS k-tile, 64 (128-byte rows, two 16x16x32 MFMA k-steps per tile) or 32 (64-byte rows, one
+// k-step: half the ring bytes, so 256x128 tiles run two blocks per CU, r05). The MFMA sequence over k is the
+// same either way, so results are bit-identical across KB.
+__device__ __forceinline__ int dma_key32(int r) { return (4 - ((r >> 2) & 3)) & 3; }  // 64-byte rows: slot = chunk ^ key
+
+template <int BM, int BN, int WGM, int WGN, int S, int EP, int KB = 64>
 __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1,
                                               unsigned bytesw) {
+  static_assert(KB == 64 || KB == 32, "k-tile depth");
   constexpr int NW = WGM * WGN, NT = NW * 64;
-  constexpr int RB = 128;
+  constexpr int RB = KB * 2;                 // LDS bytes per tile row
+  constexpr int RPI = 1024 / RB;             // rows per LDS-DMA wave-instruction (1 KB)
+  constexpr int LPR = RB / 16;               // lanes per row
+  constexpr int KSUB = KB / 32;              // 16x16x32 k-steps per tile
   constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
-  constexpr int AI = BM / NW / 8, BI = BN / NW / 8;
+  constexpr int AI = BM / NW / RPI, BI = BN / NW / RPI;
   constexpr int PER = AI + BI;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  static_assert(AI >= 1 && BI >= 1 && AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave split");
+  static_assert(AI >= 1 && BI >= 1 && AI * RPI * NW == BM && BI * RPI * NW == BN, "tile / wave split");
   static_assert(S >= 2 && S <= 4 && PER * (S - 2) <= 63, "ring");
 
   extern __shared__ __attribute__((aligned(16))) char lds[];
   HALO_STAMP(0);
 
-  int kt_begin = 0, kt_end = a.nk;
+  const int nkt = a.nk * (64 / KB);  // a.nk counts 64-deep k-tiles
+  int kt_begin = 0, kt_end = nkt;
   if (a.splits > 1) {  // split-K: blockIdx.z = k-range, raw fp32 partial sums into slab z
     const int z = blockIdx.z;
-    kt_begin = min(a.nk, z * a.kper);
-    kt_end = min(a.nk, kt_begin + a.kper);
+    kt_begin = min(nkt, z * a.kper);
+    kt_end = min(nkt, kt_begin + a.kper);
     if (!a.sk_cnt) a.out += (long)z * a.M * a.out_ld * 4;  // (the folded form writes a.sk_ws, below)
   } else if (gridDim.z > 1) {
     const long z = blockIdx.z;
@@ -1090,8 +1100,9 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WGN, wn = wave - (wave / WGN) * WGN;
-  const int g = lane >> 3, sl = lane & 7;
-  const int ce = sl ^ (((g >> 1) & 1) << 2);  // logical chunk of this lane's slot for rows with bit3 = 0
+  const int g = lane / LPR, sl = lane % LPR;
+  // logical chunk of this lane's slot (128-byte rows: for rows with bit3 = 0; 64-byte rows: every row)
+  const int ce = KB == 64 ? sl ^ (((g >> 1) & 1) << 2) : sl ^ dma_key32(g);
   const int hw_o = a.ho * a.wo;
   const int hin = a.up2 ? 2 * a.h : a.h, win = a.up2 ? 2 * a.w : a.w;
 
@@ -1099,12 +1110,12 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
   const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.in1, (short)0, (int)bytes1, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)a.weight, (short)0, (int)bytesw, 0x00020000);
 
-  // A rows of this lane: r = wave*AI*8 + j*8 + g
+  // A rows of this lane: r = (wave*AI + j)*RPI + g
   int r_img[AI], r_iy[AI], r_ix[AI], pix[AI];
   unsigned voa[AI];
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
-    const int m = m0 + (wave * AI + j) * 8 + g;
+    const int m = m0 + (wave * AI + j) * RPI + g;
     if (m < a.M) {
       const int img = m / hw_o, rem = m - img * hw_o;
       const int oy = rem / a.wo, ox = rem - oy * a.wo;
@@ -1118,13 +1129,13 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
   unsigned vob[BI];
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
-    const int nn = n0 + (wave * BI + j) * 8 + g;
-    const int ch = ce ^ (((wave * BI + j) & 1) << 1);
+    const int nn = n0 + (wave * BI + j) * RPI + g;
+    const int ch = KB == 64 ? ce ^ (((wave * BI + j) & 1) << 1) : ce;
     vob[j] = nn < a.cout ? (unsigned)nn * (unsigned)(a.wld * 2) + ch * 16 : kOOB;
   }
 
   // issue cursor (wave-uniform): filter tap, concat segment, 64-channel block within the segment
-  const int nb0 = a.c0 >> 6, nb1 = a.c1 >> 6;
+  const int nb0 = a.c0 / KB, nb1 = a.c1 / KB;  // k-tiles per concat segment and tap
   int i_tap = kt_begin / (nb0 + nb1), i_seg = 0, i_cb = kt_begin - i_tap * (nb0 + nb1);
   if (i_cb >= nb0) { i_seg = 1; i_cb -= nb0; }
   auto set_rows = [&]() {  // pixel of every A row for tap i_tap (-1 = zero padding)
@@ -1141,7 +1152,7 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
     const unsigned ldb = (unsigned)(i_seg ? a.ld1 : a.ld0) * 2u;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
-      const int ch = ce ^ (((wave * AI + j) & 1) << 1);
+      const int ch = KB == 64 ? ce ^ (((wave * AI + j) & 1) << 1) : ce;
       voa[j] = pix[j] >= 0 ? (unsigned)pix[j] * ldb + ch * 16 : kOOB;
     }
   };
@@ -1151,12 +1162,12 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
   auto issue = [&](int kt, int slot) {
     char* sb = lds + slot * STAGE;
     const __amdgpu_buffer_rsrc_t rsa = i_seg ? rs1 : rs0;
-    const int soa = i_cb * 128;
+    const int soa = i_cb * RB;
 #pragma unroll
     for (int j = 0; j < AI; ++j)
-      dma16(rsa, sb + (wave * AI + j) * 8 * RB, voa[j], soa);
+      dma16(rsa, sb + (wave * AI + j) * 1024, voa[j], soa);
 #pragma unroll
-    for (int j = 0; j < BI; ++j) dma16(rsw, sb + A_BYTES + (wave * BI + j) * 8 * RB, vob[j], kt * 128);
+    for (int j = 0; j < BI; ++j) dma16(rsw, sb + A_BYTES + (wave * BI + j) * 1024, vob[j], kt * RB);
     // advance the cursor
     if (++i_cb == (i_seg ? nb1 : nb0)) {
       i_cb = 0;
@@ -1178,7 +1189,7 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lrow = lane & 15, lq = lane >> 4;
-  const int rkey = dma_key(lrow);
+  const int rkey = KB == 64 ? dma_key(lrow) : dma_key32(lrow);
   const int nk = kt_end - kt_begin;
 
 #pragma unroll
@@ -1200,7 +1211,7 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
     const char* Ab = lds + cur * STAGE + (wm * WTM + lrow) * RB;
     const char* Bb = lds + cur * STAGE + A_BYTES + (wn * WTN + lrow) * RB;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < KSUB; ++s) {
       const int so = ((s * 4 + lq) ^ rkey) * 16;
       bf16x8 bfv[TN];
 #pragma unroll
@@ -1249,16 +1260,23 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
 // hardware admits floor(800 / (ceil(sgpr / 16) * 16 + 16)) waves per SIMD; MI355X_MICROARCH.md
 // "Residency"), so the 16-wave 128x128 tile (64 KB of LDS: two blocks fit) is built with its
 // SGPR budget capped; the others keep the compiler's allocation.
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+template <int BM, int BN, int WGM, int WGN, int S, int EP, int KB = 64>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_dma_kernel(ConvArgs a, int tiles_n, unsigned bytes0,
                                                                   unsigned bytes1, unsigned bytesw) {
-  conv_dma_body<BM, BN, WGM, WGN, S, EP>(a, tiles_n, bytes0, bytes1, bytesw);
+  conv_dma_body<BM, BN, WGM, WGN, S, EP, KB>(a, tiles_n, bytes0, bytes1, bytesw);
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+template <int BM, int BN, int WGM, int WGN, int S, int EP, int KB = 64>
 __global__ __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_num_sgpr(80))) void conv_dma_kernel_2pc(
     ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1, unsigned bytesw) {
-  conv_dma_body<BM, BN, WGM, WGN, S, EP>(a, tiles_n, bytes0, bytes1, bytesw);
+  conv_dma_body<BM, BN, WGM, WGN, S, EP, KB>(a, tiles_n, bytes0, bytes1, bytesw);
+}
+
+// two 8-wave blocks per CU (the 32-deep k-tile form): 4 waves per SIMD, <= 128 VGPRs
+template <int BM, int BN, int WGM, int WGN, int S, int EP, int KB>
+__global__ __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv_dma_kernel_2b(
+    ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1, unsigned bytesw) {
+  conv_dma_body<BM, BN, WGM, WGN, S, EP, KB>(a, tiles_n, bytes0, bytes1, bytesw);
 }
 
 // DMA-path eligibility: bf16, 16-byte-aligned 64-channel blocks, every buffer < 2 GiB.
@@ -1281,45 +1299,51 @@ bool dma_ok(const rdeic_conv_desc* d, const ConvArgs& a, unsigned& b0, unsigned&
 
 // Whether the kernel's vector epilogue runs for these arguments (the compile-time part mirrors the
 // `if constexpr` in conv_dma_kernel).
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+template <int BM, int BN, int WGM, int WGN, int S, int EP, int KB = 64>
 bool dma_vec_epilogue(const ConvArgs& a) {
   constexpr int TM = BM / WGM / 16;
-  constexpr bool fits = TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * (BM + BN) * 128;
+  constexpr bool fits = TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * (BM + BN) * KB * 2;
   return fits && (a.epi_vec || a.out_mode == 2) && epi_vec_ok(a);
 }
 
 // gn_hw: pixels per image of the GroupNorm the statistics feed; the 64-row partial blocks must not
 // straddle two images, and the epilogue must be the vector one with a statistics-capable tile.
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+template <int BM, int BN, int WGM, int WGN, int S, int EP, int KB = 64>
 int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int gn_hw, bool* fused) {
   if (a.gn_part) {
     const bool ok = a.splits > 1 && a.sk_cnt  // the split-K fold's last block writes them
                         ? a.batch == 1 && a.out_mode == 0 && gn_hw > 0 && gn_hw % 64 == 0 && BM % 64 == 0
                         : a.splits <= 1 && a.batch == 1 && a.out_mode == 0 && gn_hw > 0 && gn_hw % 64 == 0 &&
                               stats_tile_ok<BM, BN, WGM, WGM * WGN * 64, EP>() &&
-                              dma_vec_epilogue<BM, BN, WGM, WGN, S, EP>(a);
+                              dma_vec_epilogue<BM, BN, WGM, WGN, S, EP, KB>(a);
     if (!ok) a.gn_part = nullptr;
     if (fused) *fused = ok;
   }
   const int tn = cdiv(a.cout, BN);
   const long tiles = (long)cdiv(a.M, BM) * tn;
   dim3 grid((unsigned)tiles, 1, a.splits > 1 ? a.splits : a.batch);
-  constexpr int lds = S * (BM + BN) * 128;
-  if constexpr (WGM * WGN == 16 && S * (BM + BN) * 128 <= 80 * 1024)
-    hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0, b1,
-                       bw);
+  constexpr int lds = S * (BM + BN) * KB * 2;
+  if constexpr (WGM * WGN == 16 && lds <= 80 * 1024)
+    hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP, KB>), grid, dim3(WGM * WGN * 64), lds, s, a, tn,
+                       b0, b1, bw);
+  else if constexpr (KB == 32 && WGM * WGN == 8 && lds <= 80 * 1024)
+    hipLaunchKernelGGL((conv_dma_kernel_2b<BM, BN, WGM, WGN, S, EP, KB>), grid, dim3(WGM * WGN * 64), lds, s, a, tn,
+                       b0, b1, bw);
   else
-    hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0, b1, bw);
+    hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP, KB>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0,
+                       b1, bw);
   return launch_status();
 }
 
-// DMA tiles (ids 20..34; BMxBN/waves, S = ring depth):
+// DMA tiles (ids 20..39; BMxBN/waves, S = ring depth):
 //   20 256x256/8 S2, 21 256x128/8 S3, 22 128x256/8 S3, 23 128x128/4 S3, 24 128x128/4 S2,
 //   25 128x128/8 S2, 26 64x128/4 S3, 27 128x128/8 S3, 28 256x128/8 S2, 29 128x256/8 S2,
 //   30 64x128/4 S2, 31 128x64/4 S2, 32 256x256/16 S2, 33 256x128/16 S2, 34 128x128/16 S2,
 //   35 512x128/16 S2 (64x64 per wave at cout = 128: the whole 160 KB of LDS, one block per CU),
 //   36 64x128/8 S2 (32x32 per wave: twice the waves of tile 30 on grids of ~256 tiles),
-//   37 128x160/4 S2 and 38 64x160/4 S2 (N = 320 layers: two N tiles, no padded columns)
+//   37 128x160/4 S2 and 38 64x160/4 S2 (N = 320 layers: two N tiles, no padded columns),
+//   39 256x128/8 S3 with 32-deep k-tiles (72 KB: two blocks per CU, so one block's epilogue overlaps the
+//   other's k-loop; for the short-K transformer linears, r05)
 // (r04: 16-wave S3 / S4 rings for the short-K linears, 256x128 S3, 128x256 S3, 128x128 S4, were
 //  slower than these S2 tiles on every transformer linear: profiles/r04_linear_tiles.jsonl)
 // Measured (tools/dma_bench.py, one MI355X): 32 is best where a 256x256 grid fills the chip
@@ -1329,7 +1353,7 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
 // tools/tune_tiles.py; shapes missing from it use this heuristic).
 int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s, int tile,
                     int gn_hw = 0, bool* fused = nullptr) {
-  if (tile < 20 || tile > 38) {
+  if (tile < 20 || tile > 39) {
     const long zb = a.splits > 1 ? a.splits : a.batch;
     const long t128 = (long)cdiv(a.M, 128) * cdiv(a.cout, 128) * zb;
     const long t256 = (long)cdiv(a.M, 256) * cdiv(a.cout, 256) * zb;
@@ -1355,6 +1379,7 @@ int launch_dma_auto(const ConvArgs& a, unsigned b0, unsigned b1, unsigned bw, hi
     case 36: return launch_dma<64, 128, 2, 4, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
     case 37: return launch_dma<128, 160, 2, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
     case 38: return launch_dma<64, 160, 2, 2, 2, 2>(a, b0, b1, bw, s, gn_hw, fused);
+    case 39: return launch_dma<256, 128, 4, 2, 3, 2, 32>(a, b0, b1, bw, s, gn_hw, fused);
     default: return launch_dma<128, 128, 2, 2, 3, 2>(a, b0, b1, bw, s, gn_hw, fused);
   }
 }
@@ -2431,7 +2456,11 @@ __global__ __launch_bounds__(1024) void conv3x3_halo256_kernel(ConvArgs a, int t
 int g_halo256 = 0;
 
 int g_halo8 = 1;  // the 8-row halo conv where it applies (rdeic_set_conv_option(9, v))
-int g_sk_fold = 1;  // split-K reduction folded into the producer (rdeic_set_conv_option(11, v))
+// split-K reduction folded into the producer (rdeic_set_conv_option(11, v)); off by default: the last split
+// of a tile reduces it alone, so the reduction runs on one block per output tile (80 on the UNet's 8x8
+// level) instead of the reduce kernel's hundreds, and the fold's tiles are restricted to the 4- / 8-wave
+// ones; measured r05: bench 149.0 -> 133.2 img/s, fine-tune 19.0 -> 14.3 img/s (gpurun_out/r05f)
+int g_sk_fold = 0;
 
 int g_halo = 1;  // 3x3 halo conv: 0 off, 1 for GroupNorm-input convs (default), 2 for every eligible conv
 

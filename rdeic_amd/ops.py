@@ -245,14 +245,14 @@ def _gn_part_of(t: Optional[torch.Tensor], hw: int):
 # (conv_tiles.json, measured once on an MI355X by tools/tune_tiles.py): the same kernel runs for a
 # given shape in every process and on every box. Shapes missing from the table use the library's
 # built-in heuristic (tile -1). AUTOTUNE (tuning runs only) times the candidates for missing shapes.
-# Layers whose channel segments are multiples of 64 run on the LDS-DMA kernel (tile ids 20..34,
+# Layers whose channel segments are multiples of 64 run on the LDS-DMA kernel (tile ids 20..39,
 # rdeic_hip.h); the others on the register-staged tiles (0..10).
 AUTOTUNE = False
 FORCE_TILE: Optional[int] = None  # tests / tools: run every eligible conv on this tile id
 GEGLU_FUSED = True  # bf16 transformer FF: GEGLU in the projection's epilogue (conv out_mode 2)
 TILE_CANDIDATES = (0, 1, 3, 4, 6, 8, 10)
-DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31, 35, 36, 37, 38)
-ALL_TILES = (0, 1, 2, 3, 4, 6, 7, 8, 9, 10) + tuple(range(20, 39))
+DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31, 35, 36, 37, 38, 39)
+ALL_TILES = (0, 1, 2, 3, 4, 6, 7, 8, 9, 10) + tuple(range(20, 40))
 # RDEIC_TILE_TABLE: another table file (same-box A/B of tile tables, tools/table_ab.sh)
 TILE_TABLE_PATH = os.environ.get("RDEIC_TILE_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                      "conv_tiles.json")

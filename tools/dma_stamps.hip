@@ -37,14 +37,14 @@ static double pct(std::vector<double> v, double q) {
   return v.empty() ? 0 : v[(size_t)(q * (v.size() - 1))];
 }
 
-static const int BMS[] = {256, 256, 128, 128, 128, 128, 64, 128, 256, 128, 64, 128, 256, 256, 128, 512, 64, 128, 64};
-static const int BNS[] = {256, 128, 256, 128, 128, 128, 128, 128, 128, 256, 128, 64, 256, 128, 128, 128, 128, 160, 160};
+static const int BMS[] = {256, 256, 128, 128, 128, 128, 64, 128, 256, 128, 64, 128, 256, 256, 128, 512, 64, 128, 64, 256};
+static const int BNS[] = {256, 128, 256, 128, 128, 128, 128, 128, 128, 256, 128, 64, 256, 128, 128, 128, 128, 160, 160, 128};
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 65536, K = argc > 2 ? atoi(argv[2]) : 320, N = argc > 3 ? atoi(argv[3]) : 2560;
   const int tile = argc > 4 ? atoi(argv[4]) : 32;
   const int geglu = argc > 5 ? atoi(argv[5]) : 0, use_res = argc > 6 ? atoi(argv[6]) : 0;
-  if (tile < 20 || tile > 38) { fprintf(stderr, "tile 20..38\n"); return 1; }
+  if (tile < 20 || tile > 39) { fprintf(stderr, "tile 20..39\n"); return 1; }
   const int wld = (K + 63) / 64 * 64;
   const int NO = geglu ? N / 2 : N;
   bf16 *x, *wt, *res = nullptr, *out;
@@ -100,7 +100,7 @@ int main(int argc, char** argv) {
     epi.push_back((double)(q[3] - q[2]));
     tot.push_back((double)(q[3] - q[0]));
   }
-  const int nk = wld / 64;
+  const int nk = wld / (tile == 39 ? 32 : 64);
   printf("{\"shape\": [%d, %d, %d], \"tile\": %d, \"bm\": %d, \"bn\": %d, \"geglu\": %d, \"res\": %d, \"us\": %.2f, "
          "\"tflops\": %.1f, \"tiles\": %ld, \"span_cycles\": %.0f, \"cycles\": {\"issue_med\": %.0f, \"kloop_med\": %.0f, "
          "\"kloop_p90\": %.0f, \"kloop_per_ktile\": %.0f, \"epilogue_med\": %.0f, \"epilogue_p90\": %.0f, "
