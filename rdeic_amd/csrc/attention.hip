@@ -194,31 +194,46 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ q, int 
   }
 }
 
+// max over the four lanes of a query (lanes lr, lr + 16, lr + 32, lr + 48) on the gfx950 permlane swaps,
+// no LDS round trip; the raw v_max skips the NaN-quieting copies the compiler puts around a
+// builtin max of bit-cast operands (the scores are never NaN: masked keys are -inf)
+__device__ __forceinline__ float qmax4(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  float m;
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
+  auto r2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(__uint_as_float(r2[0])), "v"(__uint_as_float(r2[1])));
+  return m;
+}
+
 // bf16 head dims 16 / 32 (the control branch's d=16 heads): the transposed formulation keeps P in
 // registers. S^T = K Q^T gives each lane ONE query (column lr) and 16 of the tile's 64 keys, so the
 // running max / sum need two cross-lane steps per tile and no LDS round trip; P^T is then already
 // the B operand of O^T += V^T P^T. The 32-key contraction of each PV MFMA runs in a permuted key
 // order (k slot 8*lg + j <-> key 32s + 16*(j>>2) + 4*lg + (j&3)); V^T is read in the same order.
 // O^T lands as lane = query, 4 consecutive head-dim values per lane -> one 8-byte store.
+//
+// d = 16 (the kernel is VALU-bound on the softmax): Q is scaled by scale*log2(e) once and split
+// hi + lo (two bf16 whose sum is the fp32 product to ~2^-17) into the two k halves of one
+// v_mfma_f32_16x16x32_bf16 against K duplicated along k, and the accumulator starts at -m (the
+// running max in scaled units). The MFMA then emits the exp2 argument itself: no per-score fma,
+// products exact and summed in fp32 as before.
+// Staging: the next tile's K / V chunks are loaded into registers while this tile computes.
 template <int DH, int NQ, int KTL>
-__global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict__ q, int ldq,
-                                                         const bf16* __restrict__ k, int ldk,
-                                                         const bf16* __restrict__ v, int ldv, bf16* __restrict__ o,
-                                                         int ldo, int heads, int lq, int lk, float scale_log2,
-                                                         int kv_bcast) {
-  // NQ groups of 16 queries per wave share every staged K/V tile of KTL keys (fewer barriers and
-  // LDS fills per score); the 2-stage barrier pattern is the generic kernel's.
+__device__ __forceinline__ void attn_small_body(const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k,
+                                                int ldk, const bf16* __restrict__ v, int ldv, bf16* __restrict__ o,
+                                                int ldo, int heads, int lq, int lk, float scale_log2, int kv_bcast) {
+  // NQ groups of 16 queries per wave share every staged K/V tile of KTL keys
   static_assert(DH == 16 || DH == 32, "small-head kernel");
-  // QK^T contraction: d = 16 on the k = 16 MFMA (v_mfma_f32_16x16x16_bf16, half the k = 32 form's
-  // cycles and no zero padding), d = 32 on the k = 32 one
-  constexpr bool K16 = DH == 16;
-  constexpr int DP = K16 ? 16 : 32;
-  constexpr int KROW = DP + 8;   // K tile row stride (elements)
+  constexpr bool HL = DH == 16;
+  constexpr int KROW = DH + 8;   // K tile row stride (elements)
   constexpr int VROW = KTL + 8;  // V^T tile row stride
   constexpr int NDT = DH / 16;
   constexpr int CPR = DH / 8;    // 16-byte chunks per K/V row
   constexpr int NT = KTL / 16;   // S^T sub-tiles per key tile
   constexpr int NS = KTL / 32;   // PV MFMAs per key tile (per d tile)
+  constexpr int NCH = KTL * CPR;
+  constexpr int NPT = (NCH + 255) / 256;  // staged chunks per thread
   __shared__ __attribute__((aligned(16))) bf16 Ks[KTL * KROW];
   __shared__ __attribute__((aligned(16))) bf16 Vt[DH * VROW];
 
@@ -232,63 +247,78 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
   const bf16* kb = k + kvb * lk * ldk + h * DH;
   const bf16* vb = v + kvb * lk * ldv + h * DH;
 
-  bf16x8 qf[NQ];  // K16: the low 4 hold Q[query lr][d = 4 lg .. 4 lg + 3]
+  // HL: lanes lg = 0, 1 hold hi(Q')[query lr][d = 8 lg ..], lanes lg = 2, 3 lo(Q') of the same d
+  bf16x8 qf[NQ];
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
     const int myq = q0 + (wave * NQ + g) * 16 + lr;
 #pragma unroll
     for (int e = 0; e < 8; ++e) qf[g][e] = (bf16)0.f;
-    if constexpr (K16) {
+    if constexpr (HL) {
       if (myq < lq) {
-        const bf16x4 q4 = *reinterpret_cast<const bf16x4*>(qb + (long)myq * ldq + 4 * lg);
+        const bf16x8 q8 = *reinterpret_cast<const bf16x8*>(qb + (long)myq * ldq + 8 * (lg & 1));
 #pragma unroll
-        for (int e = 0; e < 4; ++e) qf[g][e] = q4[e];
+        for (int e = 0; e < 8; ++e) {
+          const float x = (float)q8[e] * scale_log2;
+          const bf16 hi = (bf16)x;
+          qf[g][e] = (lg >> 1) ? (bf16)(x - (float)hi) : hi;
+        }
       }
     } else {
       if (myq < lq && 8 * lg < DH) qf[g] = *reinterpret_cast<const bf16x8*>(qb + (long)myq * ldq + 8 * lg);
-    }
-  }
-  if constexpr (DP > DH) {  // K pad columns: zero once, the staging never writes them
-    for (int idx = tid; idx < KTL * (DP - DH); idx += 256) {
-      const int kr = idx / (DP - DH), dd = DH + idx % (DP - DH);
-      Ks[kr * KROW + dd] = (bf16)0.f;
     }
   }
   f32x4 oacc[NQ][NDT];
   // row sums on the matrix core (ONES . P^T, as the d64 kernel): each lane gets its query's sum of
   // the bf16 probabilities, complete, with no per-score add and no cross-lane reduction
   f32x4 lsum[NQ];
-  float m_run[NQ];
+  float m_run[NQ];  // HL: scaled units, valid from the first tile on; else raw scores, -inf at start
+  f32x4 minit[NQ];  // HL: {-m, -m, -m, -m}, the QK accumulator's start value
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
-    m_run[g] = -INFINITY;
+    m_run[g] = HL ? 0.f : -INFINITY;
+    minit[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     lsum[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < NDT; ++u) oacc[g][u] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
+  bf16x8 kreg[NPT], vreg[NPT];
+  auto fetch = [&](int key0) {
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int cidx = tid + 256 * j;
+      const int kr = cidx / CPR, ch = cidx - kr * CPR;
+      const int key = key0 + kr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { kreg[j][e] = (bf16)0.f; vreg[j][e] = (bf16)0.f; }
+      if (cidx < NCH && key < lk) {
+        kreg[j] = *reinterpret_cast<const bf16x8*>(kb + (long)key * ldk + ch * 8);
+        vreg[j] = *reinterpret_cast<const bf16x8*>(vb + (long)key * ldv + ch * 8);
+      }
+    }
+  };
+
   const int ntiles = (lk + KTL - 1) / KTL;
+  fetch(0);
   for (int kt = 0; kt < ntiles; ++kt) {
     const int key0 = kt * KTL;
     __syncthreads();
-    for (int cidx = tid; cidx < KTL * CPR; cidx += 256) {
-      const int kr = cidx / CPR, ch = cidx - kr * CPR;
-      const int key = key0 + kr;
-      bf16x8 kv, vv;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { kv[e] = (bf16)0.f; vv[e] = (bf16)0.f; }
-      if (key < lk) {
-        kv = *reinterpret_cast<const bf16x8*>(kb + (long)key * ldk + ch * 8);
-        vv = *reinterpret_cast<const bf16x8*>(vb + (long)key * ldv + ch * 8);
+    for (int j = 0; j < NPT; ++j) {
+      const int cidx = tid + 256 * j;
+      if (cidx < NCH) {
+        const int kr = cidx / CPR, ch = cidx - kr * CPR;
+        *reinterpret_cast<bf16x8*>(&Ks[kr * KROW + ch * 8]) = kreg[j];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VROW + kr] = vreg[j][e];
       }
-      *reinterpret_cast<bf16x8*>(&Ks[kr * KROW + ch * 8]) = kv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VROW + kr] = vv[e];
     }
     __syncthreads();
+    if (kt + 1 < ntiles) fetch(key0 + KTL);
 
 #pragma unroll
     for (int g = 0; g < NQ; ++g) {
@@ -296,19 +326,15 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
       f32x4 sacc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        if constexpr (K16) {
-          typedef short s4v __attribute__((ext_vector_type(4)));
-          const bf16x4 kf = *reinterpret_cast<const bf16x4*>(&Ks[(16 * t + lr) * KROW + 4 * lg]);
-          const bf16x4 q4 = __builtin_shufflevector(qf[g], qf[g], 0, 1, 2, 3);
-          sacc[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4v, kf), __builtin_bit_cast(s4v, q4),
-                                                              f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        if constexpr (HL) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(16 * t + lr) * KROW + 8 * (lg & 1)]);
+          sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g], minit[g], 0, 0, 0);
         } else {
           const bf16x8 kf = *reinterpret_cast<const bf16x8*>(&Ks[(16 * t + lr) * KROW + 8 * lg]);
           sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
       }
-      // the running max stays in raw-score units (scale > 0): one fma per score folds the scale
-      // and the max subtraction; only the last, partial key tile pays for the mask
+      // only the last, partial key tile pays for the mask
       if (key0 + KTL > lk) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -321,31 +347,48 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sacc[t][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       // deferred rescale: the running max moves only when a score exceeds it by more than 2^8 in
       // exp2 units (probabilities <= 256 stay exact enough in fp32 / bf16), so most tiles skip the
       // alpha exp and the accumulator rescale
-      if ((mx - m_run[g]) * scale_log2 > 8.f) {
-        const float alpha = __builtin_amdgcn_exp2f((m_run[g] - mx) * scale_log2);
-        m_run[g] = mx;
-        lsum[g] *= alpha;
-#pragma unroll
-        for (int u = 0; u < NDT; ++u) oacc[g][u] *= alpha;
-      }
-      const float mneg = -m_run[g] * scale_log2;
       bf16x8 pf[NS];
-      // the score scaling two at a time (v_pk_fma_f32): this kernel is VALU-bound on the softmax
-      typedef float f2v __attribute__((ext_vector_type(2)));
-      const f2v sc2 = {scale_log2, scale_log2}, mn2 = {mneg, mneg};
+      if constexpr (HL) {
+        // sacc already holds scaled score - m. The cross-lane max runs only when some lane of the
+        // wave needs a move (a wave-uniform branch) or on the first tile, which sets m to its max;
+        // a query whose four lanes all stay within 2^8 shifts by exactly 0 there (alpha = 1)
+        if (kt == 0 || __builtin_amdgcn_ballot_w64(mx > 8.f)) {
+          mx = qmax4(mx);
+          const float d = (kt == 0 || mx > 8.f) ? mx : 0.f;
+          const float alpha = kt == 0 ? 0.f : __builtin_amdgcn_exp2f(-d);
+          m_run[g] += d;
+          minit[g] = f32x4{-m_run[g], -m_run[g], -m_run[g], -m_run[g]};
+          lsum[g] *= alpha;
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+          for (int u = 0; u < NDT; ++u) oacc[g][u] *= alpha;
 #pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-          const f2v z = __builtin_elementwise_fma(f2v{sacc[t][i], sacc[t][i + 1]}, sc2, mn2);
-          pf[t >> 1][(t & 1) * 4 + i] = (bf16)__builtin_amdgcn_exp2f(z[0]);
-          pf[t >> 1][(t & 1) * 4 + i + 1] = (bf16)__builtin_amdgcn_exp2f(z[1]);
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sacc[t][i] -= d;
         }
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pf[t >> 1][(t & 1) * 4 + i] = (bf16)__builtin_amdgcn_exp2f(sacc[t][i]);
+      } else {
+        mx = qmax4(mx);
+        if ((mx - m_run[g]) * scale_log2 > 8.f) {
+          const float alpha = __builtin_amdgcn_exp2f((m_run[g] - mx) * scale_log2);
+          m_run[g] = mx;
+          lsum[g] *= alpha;
+#pragma unroll
+          for (int u = 0; u < NDT; ++u) oacc[g][u] *= alpha;
+        }
+        const float mneg = -m_run[g] * scale_log2;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            pf[t >> 1][(t & 1) * 4 + i] = (bf16)__builtin_amdgcn_exp2f(__builtin_fmaf(sacc[t][i], scale_log2, mneg));
+      }
 #pragma unroll
       for (int s2 = 0; s2 < NS; ++s2) lsum[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[s2], lsum[g], 0, 0, 0);
       // O^T[d][q] += sum_k V^T[d][key(k)] P^T[key(k)][q]
@@ -376,6 +419,24 @@ __global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict_
       }
     }
   }
+}
+
+template <int DH, int NQ, int KTL>
+__global__ __launch_bounds__(256) void attn_small_kernel(const bf16* __restrict__ q, int ldq,
+                                                         const bf16* __restrict__ k, int ldk,
+                                                         const bf16* __restrict__ v, int ldv, bf16* __restrict__ o,
+                                                         int ldo, int heads, int lq, int lk, float scale_log2,
+                                                         int kv_bcast) {
+  attn_small_body<DH, NQ, KTL>(q, ldq, k, ldk, v, ldv, o, ldo, heads, lq, lk, scale_log2, kv_bcast);
+}
+
+// d = 16, 16 queries per wave: held to 64 VGPRs so 8 blocks fit a CU (at 66
+// only 7 do, and a 4096-query launch of 4096 blocks then runs 2.3 rounds of 1792 instead of 2 of 2048)
+template <int DH, int NQ, int KTL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void attn_small_kernel_o8(
+    const bf16* __restrict__ q, int ldq, const bf16* __restrict__ k, int ldk, const bf16* __restrict__ v, int ldv,
+    bf16* __restrict__ o, int ldo, int heads, int lq, int lk, float scale_log2, int kv_bcast) {
+  attn_small_body<DH, NQ, KTL>(q, ldq, k, ldk, v, ldv, o, ldo, heads, lq, lk, scale_log2, kv_bcast);
 }
 
 template <typename T>
@@ -1306,19 +1367,24 @@ int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, i
                          ldv, (bf16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_bcast);
       return launch_status();
     }
-    // small heads: register-resident P (A/B switch: RDEIC_ATTN_SMALL=0 -> generic kernel)
-    static const bool small_on = !getenv("RDEIC_ATTN_SMALL") || atoi(getenv("RDEIC_ATTN_SMALL")) != 0;
-    if ((dh == 16 || dh == 32) && small_on && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0) {
+    // small heads: register-resident P. A/B switch RDEIC_ATTN_SMALL: 0 generic kernel, 1 one 16-query
+    // group per wave over 64-key tiles, 2 two groups over 128-key tiles, 3 two groups over 64-key
+    // tiles; unset: d = 16 takes 3 from 2048 queries on (r05 A/B, same box: 338 / 393 TF against
+    // 310 / 355 for 1 at L = 4096 / 16384), 1 below (half the grid of 3 there)
+    static const int sel = getenv("RDEIC_ATTN_SMALL") ? atoi(getenv("RDEIC_ATTN_SMALL")) : -1;
+    if ((dh == 16 || dh == 32) && sel != 0 && ldo % 4 == 0 && ((uintptr_t)o) % 8 == 0) {
       const float sl2 = scale * 1.4426950408889634f;
-      // RDEIC_ATTN_SMALL=2: 2 query groups per wave over 128-key tiles on long sequences (A/B: 2.38 vs
-      // 2.22 ms/step for the default 1 x 64 — the kernel is VALU-bound on the softmax, not on staging)
-      const bool big = lq >= 1024 && getenv("RDEIC_ATTN_SMALL") && atoi(getenv("RDEIC_ATTN_SMALL")) == 2;
 #define SMALL_LAUNCH(D, NQ, KTL)                                                                                  \
   hipLaunchKernelGGL((attn_small_kernel<D, NQ, KTL>), dim3((lq + 64 * NQ - 1) / (64 * NQ), batch * heads),       \
                      dim3(256), 0, s, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, \
                      heads, lq, lk, sl2, kv_bcast)
-      if (dh == 16 && big) SMALL_LAUNCH(16, 2, 128);
-      else if (dh == 16) SMALL_LAUNCH(16, 1, 64);
+      const bool big = lq >= 1024 && sel == 2;
+      if (dh == 16 && (sel == 3 || (sel < 0 && lq >= 2048))) SMALL_LAUNCH(16, 2, 64);
+      else if (dh == 16 && big) SMALL_LAUNCH(16, 2, 128);
+      else if (dh == 16)
+        hipLaunchKernelGGL((attn_small_kernel_o8<16, 1, 64>), dim3((lq + 63) / 64, batch * heads), dim3(256), 0, s,
+                           (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, heads, lq,
+                           lk, sl2, kv_bcast);
       else if (big) SMALL_LAUNCH(32, 2, 128);
       else SMALL_LAUNCH(32, 1, 64);
 #undef SMALL_LAUNCH

@@ -163,7 +163,7 @@ def _ref_attn(q, k, v, heads, dh, scale):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("heads,dh,lq,lk", [(5, 64, 256, 256), (4, 16, 300, 300), (10, 64, 64, 77), (16, 16, 64, 77),
                                            (4, 16, 4096, 4096), (8, 32, 130, 200), (2, 16, 1100, 77), (2, 32, 1030, 300),
-                                           (20, 64, 100, 33)])
+                                           (20, 64, 100, 33), (2, 16, 2300, 2100), (3, 16, 2100, 77)])
 def test_attention(gpu, dtype, heads, dh, lq, lk):
     from rdeic_amd import ops
     g = torch.Generator().manual_seed(heads * dh + lq)
@@ -181,6 +181,28 @@ def test_attention(gpu, dtype, heads, dh, lq, lk):
     torch.cuda.synchronize()
     rt, at = (2e-5, 2e-5) if dtype == torch.float32 else (3e-2, 3e-2)
     torch.testing.assert_close(out.float().cpu().view(b, lq, -1), ref, rtol=rt, atol=at)
+
+
+@pytest.mark.parametrize("lq,lk", [(300, 1000), (2300, 2100)])
+def test_attention_d16_running_max_moves(gpu, lq, lk):
+    """d = 16 kernels (one and two query groups per wave): scores that grow along the keys, so the
+    running max moves past its 2^8 slack many times (the ballot-gated rescale), plus a large
+    dynamic range; bf16 against the fp32 reference."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(5)
+    b, heads, dh = 2, 4, 16
+    q = torch.randn(b, lq, heads * dh, generator=g) * 3
+    ramp = torch.linspace(0.2, 6.0, lk).view(1, lk, 1)
+    k = torch.randn(b, lk, heads * dh, generator=g) * ramp
+    v = torch.randn(b, lk, heads * dh, generator=g)
+    scale = dh ** -0.5
+    qb, kb, vb = q.to(torch.bfloat16), k.to(torch.bfloat16), v.to(torch.bfloat16)
+    ref = _ref_attn(qb.float(), kb.float(), vb.float(), heads, dh, scale)
+    qd, kd, vd = (t.cuda().view(-1, heads * dh) for t in (qb, kb, vb))
+    out = torch.empty_like(qd)
+    ops.attention(qd, kd, vd, out, batch=b, heads=heads, lq=lq, lk=lk, dh=dh, scale=scale)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.float().cpu().view(b, lq, -1), ref, rtol=3e-2, atol=3e-2)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
