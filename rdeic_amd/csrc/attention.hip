@@ -626,24 +626,34 @@ __global__ __launch_bounds__(256) void attn64_kernel(const bf16* __restrict__ q,
             if (key0 + 16 * t + 4 * g + i >= lk) st[u][t][i] = -INFINITY;
     }
     bf16x8 pf[2][2];
-    bool rescale = false;
     float alpha[2];
+    // lane-local maxima first: the cross-lane max (permlane swaps) and the running-max move run only
+    // when some lane of the wave exceeds its query's running max by the 2^8 slack (a wave-uniform
+    // branch); a query inside the slack there keeps its max (alpha = 1), as when the branch is skipped
+    float mx[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float mx = st[u][0][0];
+      mx[u] = st[u][0][0];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[u][t][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float ms = mx * scale_log2;
+        for (int i = 0; i < 4; ++i) mx[u] = fmaxf(mx[u], st[u][t][i]);
       alpha[u] = 1.f;
-      if (ms > m_run[u] + 8.f) {
-        alpha[u] = __builtin_amdgcn_exp2f(m_run[u] - ms);
-        m_run[u] = ms;
-        rescale = true;
+    }
+    const bool rescale = __builtin_amdgcn_ballot_w64(mx[0] * scale_log2 > m_run[0] + 8.f ||
+                                                     mx[1] * scale_log2 > m_run[1] + 8.f) != 0;
+    if (rescale) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float ms = qmax4(mx[u]) * scale_log2;
+        if (ms > m_run[u] + 8.f) {
+          alpha[u] = __builtin_amdgcn_exp2f(m_run[u] - ms);
+          m_run[u] = ms;
+        }
       }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
       const float nm = -m_run[u];
       float ps = 0.f;
 #pragma unroll
@@ -874,24 +884,34 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
             if (key0 + 16 * t + 4 * g + i >= lk) st[u][t][i] = -INFINITY;
     }
     bf16x8 pf[2][2];
-    bool rescale = false;
     float alpha[2];
+    // lane-local maxima first: the cross-lane max (permlane swaps) and the running-max move run only
+    // when some lane of the wave exceeds its query's running max by the 2^8 slack (a wave-uniform
+    // branch); a query inside the slack there keeps its max (alpha = 1), as when the branch is skipped
+    float mx[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float mx = st[u][0][0];
+      mx[u] = st[u][0][0];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[u][t][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float ms = mx * scale_log2;
+        for (int i = 0; i < 4; ++i) mx[u] = fmaxf(mx[u], st[u][t][i]);
       alpha[u] = 1.f;
-      if (ms > m_run[u] + 8.f) {
-        alpha[u] = __builtin_amdgcn_exp2f(m_run[u] - ms);
-        m_run[u] = ms;
-        rescale = true;
+    }
+    const bool rescale = __builtin_amdgcn_ballot_w64(mx[0] * scale_log2 > m_run[0] + 8.f ||
+                                                     mx[1] * scale_log2 > m_run[1] + 8.f) != 0;
+    if (rescale) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float ms = qmax4(mx[u]) * scale_log2;
+        if (ms > m_run[u] + 8.f) {
+          alpha[u] = __builtin_amdgcn_exp2f(m_run[u] - ms);
+          m_run[u] = ms;
+        }
       }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
       const float nm = -m_run[u];
 #pragma unroll
       for (int c = 0; c < 2; ++c)
@@ -899,7 +919,7 @@ __global__ __launch_bounds__(256) void attn64_dma_kernel(const bf16* __restrict_
         for (int j = 0; j < 8; ++j)
           pf[u][c][j] = (bf16)__builtin_amdgcn_exp2f(fmaf(st[u][2 * c + (j >> 2)][j & 3], scale_log2, nm));
     }
-    if (__any(rescale)) {
+    if (rescale) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
 #pragma unroll
