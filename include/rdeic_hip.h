@@ -133,6 +133,12 @@ int rdeic_set_conv_path(int32_t path);
  *        measured 2-3% slower than the 8-row form); bit-identical outputs either way;
  * key 11: split-K reduction (and GroupNorm statistics) folded into the producing launch (1) / a separate
  *        reduce (and statistics) launch (0, default: the fold measured slower); bit-identical either way;
+ * key 12: the persistent short-K linear (bf16 1x1 projections, K a multiple of 32 and >= 256, output plain
+ *        or GEGLU, LayerNorm fold / bias, no residual / emb / activation / GroupNorm, >= 2048 rows): one
+ *        block per CU walks 256 x 128 tiles and runs each tile's epilogue beside the next tile's MFMAs.
+ *        0 off (default: measured slower, its 3-slot ring of 32-deep k-tiles is latency-bound), 1 where
+ *        no tile is named, 2 also over a named tile 20..39; tile 40 of rdeic_conv2d_tile names it.
+ *        Bit-identical to the LDS-DMA tiles.
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way
  * (keys 0-5; 6 and 8 change fp32 rounding only). */
 int rdeic_set_conv_option(int32_t key, int32_t value);
@@ -347,6 +353,7 @@ int rdeic_prof_start(int32_t capacity, int32_t every);
 #define RDEIC_COUNT_LN_FUSED 4     /* rdeic_layernorm_rowstats (LayerNorm folded into the next linear) */
 #define RDEIC_COUNT_SPLITK 5       /* rdeic_conv2d_splitk launches that ran split (partial pass + reduce) */
 #define RDEIC_COUNT_HALO256 6      /* conv3x3_halo256_kernel (the 256-channel halo conv, cout % 256 == 0) */
+#define RDEIC_COUNT_LPERSIST 7     /* linear_persist_kernel (the persistent short-K linear, option 12) */
 #define RDEIC_COUNT_KINDS 8
 int64_t rdeic_launch_count(int32_t kind);
 /* Per-row LayerNorm statistics (attention.py:273-285, torch.nn.LayerNorm: biased variance, eps) of

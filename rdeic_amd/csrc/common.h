@@ -50,6 +50,28 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return 0.5f * x * (1.0f + copysignf(e, x));
 }
 
+// Two values at a time on the packed-f32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of
+// work per issue). For epilogues, which run with no MFMA in flight; beside MFMAs packed f32 is an anti-lever
+// (MI355X_MICROARCH.md, constants table).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+// gelu_fast on a pair: the same A&S 7.1.26 erf, the polynomial and the affine steps packed, the rcp / exp scalar
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f32x2 d = pk_fma(z, f32x2{0.3275911f, 0.3275911f}, f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = pk_fma(f32x2{1.061405429f, 1.061405429f}, t, f32x2{-1.453152027f, -1.453152027f});
+  p = pk_fma(p, t, f32x2{1.421413741f, 1.421413741f});
+  p = pk_fma(p, t, f32x2{-0.284496736f, -0.284496736f});
+  p = pk_fma(p, t, f32x2{0.254829592f, 0.254829592f});
+  p *= t;
+  const f32x2 a = z * z * -1.4426950408889634f;  // exp(-z^2) = exp2(-z^2 log2 e)
+  const f32x2 ex = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  const f32x2 e = pk_fma(-p, ex, f32x2{1.0f, 1.0f});  // erf(|x| / sqrt 2)
+  const f32x2 se = {__builtin_copysignf(e.x, x.x), __builtin_copysignf(e.y, x.y)};
+  return (x * 0.5f) * (se + 1.0f);
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -245,8 +245,14 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
           c1 = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4);
         }
         const float cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        // v = rstd * (v - mean * colsum), two columns per packed fma / mul
+        const f32x2 nm = {-ms.x, -ms.x}, rs = {ms.y, ms.y};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = ms.y * (v[e] - ms.x * cs[e]);
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 r = rs * pk_fma(nm, f32x2{cs[e], cs[e + 1]}, f32x2{v[e], v[e + 1]});
+          v[e] = r.x;
+          v[e + 1] = r.y;
+        }
       }
       if (a.bias) {
         float4 b0 = bh[0], b1 = bh[1];
@@ -256,7 +262,11 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
         }
         const float bs[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bs[e];
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 r = f32x2{v[e], v[e + 1]} + f32x2{bs[e], bs[e + 1]};
+          v[e] = r.x;
+          v[e + 1] = r.y;
+        }
       }
       if (a.emb) {
         const float* em = a.emb + (long)(m / hw_o) * a.emb_ld + nn;
@@ -271,9 +281,12 @@ __device__ __forceinline__ void epilogue_vec(const f32x4 (&acc)[BM / WGM / 16][B
         // are rounded to bf16 first, as the unfused projection + rdeic_geglu see them.
         bf16 gv[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xv = to_f32(from_f32<bf16>(v[e])), gt = to_f32(from_f32<bf16>(v[4 + e]));
-          gv[e] = from_f32<bf16>(xv * gelu_fast(gt));
+        for (int e = 0; e < 4; e += 2) {
+          const f32x2 xv = {to_f32(from_f32<bf16>(v[e])), to_f32(from_f32<bf16>(v[e + 1]))};
+          const f32x2 gt = {to_f32(from_f32<bf16>(v[4 + e])), to_f32(from_f32<bf16>(v[5 + e]))};
+          const f32x2 r = xv * gelu_fast2(gt);
+          gv[e] = from_f32<bf16>(r.x);
+          gv[e + 1] = from_f32<bf16>(r.y);
         }
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + (nn >> 1)) =
             *reinterpret_cast<uint2*>(gv);
@@ -2453,6 +2466,261 @@ __global__ __launch_bounds__(1024) void conv3x3_halo256_kernel(ConvArgs a, int t
 
 // the 256-channel halo conv where it applies (rdeic_set_conv_option(10, v)); off by default: measured 2-3%
 // slower than halo8 on every VAE cout >= 256 shape and -0.6% on the bench (profiles/r05_halo256_ab.txt)
+// ============================================================================================
+// Persistent short-K linear (r05, option 12): the transformer's 1x1 projections with K = 320..1280 (GEGLU
+// 320 -> 2560 etc., LayerNorm-folded q/k/v). In the per-tile kernels their fixed cost is the epilogue
+// (26k of 42k cycles of a 256x256 GEGLU tile, tools/dma_stamps.hip), which no MFMA work overlaps. Here one
+// 512-thread block per CU walks its tiles (256 x 128, 8 waves of 64 x 64, 32-deep k-tiles through a 3-slot
+// LDS-DMA ring that runs on across tile boundaries). At the end of a tile's k-loop the accumulators get the
+// LayerNorm fold and the bias, are rounded to bf16 and parked in LDS; during the NEXT tile's k-loop every
+// thread turns one parked 8-column chunk per k-tile into output (GEGLU x * gelu(g) or a plain copy) and
+// stores it, so the epilogue's VALU and stores run beside that tile's MFMAs. Same MFMA sequence over k and
+// the same fp32 epilogue arithmetic as the LDS-DMA tiles (LN fold, + bias, round to bf16; GEGLU on the bf16
+// halves): outputs are bit-identical to tile 32 (test_kernels_gpu.py::test_linear_persistent_bit_identical).
+// ============================================================================================
+namespace lp {
+constexpr int BM = 256, BN = 128, WGN = 2, NW = 8, NT = NW * 64;
+constexpr int KB = 32, RB = KB * 2, RPI = 1024 / RB, LPR = RB / 16, S = 3;
+constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB, RING = S * STAGE;
+constexpr int AI = BM / NW / RPI, BI = BN / NW / RPI, PER = AI + BI;
+constexpr int WTM = 64, WTN = 64, TM = WTM / 16, TN = WTN / 16;
+constexpr int PROW = BN * 2 + 16;  // parked bf16 row (+16 B: bank spread of the chunk reads)
+constexpr int CPR = BN / 8;        // 8-column chunks per row
+constexpr int NCHUNK = BM * CPR / NT;
+constexpr int PARK = BM * PROW;
+// per-tile epilogue operands, LDS-DMA'd with the tile's first k-tile (two buffers: the next tile's arrive before
+// this one parks): LayerNorm (mean, rstd) of the 256 rows, column sums and bias of the 128 columns
+constexpr int EPI = BM * 8 + BN * 4 * 2;
+constexpr int LDS = RING + PARK + 2 * EPI;
+static_assert(AI * RPI * NW == BM && BI * RPI * NW == BN && NCHUNK * NT == BM * CPR, "tile split");
+static_assert(BM * 8 == 2 * 1024 && BN * 4 * 2 == 1024, "epilogue operands: 3 LDS-DMA wave-instructions");
+static_assert(LDS <= 160 * 1024, "one block per CU");
+}  // namespace lp
+
+// Every vector-memory op of this kernel is counted (wave-uniform): the k-tile and epilogue-operand LDS-DMAs and
+// the output stores (buffer stores, issued whole-wave, out-of-range lanes discarded by the descriptor), so the
+// wait for ring slot gi is exactly "all but the ops issued after it" (vmcnt returns in issue order).
+template <bool GEGLU>
+__global__ __launch_bounds__(lp::NT) void linear_persist_kernel(ConvArgs a, int tiles_n, int ntiles, unsigned bytes0,
+                                                                unsigned bytesw, unsigned bytes_out) {
+  using namespace lp;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const park = lds + RING;
+  char* const epi = park + PARK;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave - (wave / WGN) * WGN;
+  const int g = lane / LPR, sl = lane % LPR;
+  const int ce = sl ^ dma_key32(g);
+  // XCD-aware block order (as conv_dma_body): an XCD's blocks take consecutive tile ids, so they share A rows
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int my_tiles = wgid < ntiles ? (ntiles - 1 - wgid) / nwg + 1 : 0;
+  const int nk = a.c0 / KB;
+  const int total = my_tiles * nk;
+  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0, (int)bytes0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)a.weight, (short)0, (int)bytesw, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rso = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)bytes_out, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.ln_rows, (short)0, a.ln_rows ? (int)(a.M * 8u) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.ln_cs, (short)0, a.ln_rows ? (int)(a.cout * 4u) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bias, (short)0, a.bias ? (int)(a.cout * 4u) : 0, 0x00020000);
+  const unsigned lda = (unsigned)a.ld0 * 2u, ldw = (unsigned)a.wld * 2u;
+
+  int issued = 0;  // vector-memory ops this wave has issued
+  int mark[S];     // issued count right after ring slot s's k-tile was issued
+  auto issue = [&](int gi) {  // block-local k-iteration gi -> (tile, k-tile) into ring slot gi % S
+    const int lt = gi / nk, kt = gi - lt * nk;
+    const int tile = wgid + lt * nwg;
+    const int mt = tile / tiles_n, nt = tile - mt * tiles_n;
+    char* sb = lds + (gi % S) * STAGE;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int m = mt * BM + (wave * AI + j) * RPI + g;
+      dma16(rs0, sb + (wave * AI + j) * 1024, m < a.M ? (unsigned)m * lda + ce * 16 : kOOB, kt * RB);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int nn = nt * BN + (wave * BI + j) * RPI + g;
+      dma16(rsw, sb + A_BYTES + (wave * BI + j) * 1024, nn < a.cout ? (unsigned)nn * ldw + ce * 16 : kOOB, kt * RB);
+    }
+    issued += PER;
+    if (kt == 0 && wave < 4) {  // the tile's epilogue operands into epi buffer lt & 1, one op on waves 0..3
+      char* eb = epi + (lt & 1) * EPI;
+      if (wave < 2) {  // LayerNorm rows: 16 B per lane = rows 2 l, 2 l + 1
+        const int m = mt * BM + wave * 128 + 2 * lane;
+        const unsigned vo = (unsigned)(mt * BM + wave * 128) * 8u + lane * 16;
+        dma16(rsl, eb + wave * 1024, m < a.M ? vo : kOOB, 0);
+      } else {  // wave 2 lanes 0-31: column sums at eb + 2048; wave 3 lanes 32-63: bias at eb + 2560 (4 columns a lane)
+        const int nn = nt * BN + (lane & 31) * 4;
+        const unsigned vo = nn < a.cout ? (unsigned)nn * 4u : kOOB;
+        if (wave == 2) {
+          if (lane < 32) dma16(rsc, eb + 2048, vo, 0);
+        } else {
+          if (lane >= 32) dma16(rsb, eb + 2048, vo, 0);
+        }
+      }
+      ++issued;
+    }
+    mark[gi % S] = issued;
+  };
+
+  const int lr = lane & 15, lq = lane >> 4;
+  const int rkey = dma_key32(lr);
+  const int so = (lq ^ rkey) * 16;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one parked chunk (row pr, columns cc*8 .. +7) of tile ptile -> output (a buffer store, issued by the whole wave)
+  auto chunk = [&](int ptile, int c) {
+    const int id = tid + c * NT;
+    const int pr = id / CPR, cc = id - pr * CPR;
+    const int mt = ptile / tiles_n, nt = ptile - mt * tiles_n;
+    const int m = mt * BM + pr, nn = nt * BN + cc * 8;
+    const bool ok = m < a.M && nn < a.cout;
+    const uint4 raw = *reinterpret_cast<const uint4*>(park + pr * PROW + cc * 16);
+    if constexpr (GEGLU) {
+      bf16 hv[8];
+      *reinterpret_cast<uint4*>(hv) = raw;
+      bf16 gv[4];
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const f32x2 r = f32x2{to_f32(hv[e]), to_f32(hv[e + 1])} * gelu_fast2(f32x2{to_f32(hv[4 + e]), to_f32(hv[5 + e])});
+        gv[e] = from_f32<bf16>(r.x);
+        gv[e + 1] = from_f32<bf16>(r.y);
+      }
+      typedef unsigned u2 __attribute__((ext_vector_type(2)));
+      const uint2 gw = *reinterpret_cast<uint2*>(gv);
+      __builtin_amdgcn_raw_buffer_store_b64(u2{gw.x, gw.y}, rso,
+                                            ok ? (unsigned)((long)m * a.out_ld + (nn >> 1)) * 2u : kOOB, 0, 0);
+    } else {
+      typedef unsigned u4 __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(u4{raw.x, raw.y, raw.z, raw.w}, rso,
+                                             ok ? (unsigned)((long)m * a.out_ld + nn) * 2u : kOOB, 0, 0);
+    }
+    ++issued;
+  };
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < total) issue(s);
+
+  int kt = 0, lt = 0, ptile = -1;
+  for (int gi = 0; gi < total; ++gi) {
+    wait_vm_rt(issued - mark[gi % S]);  // at most a store + the next slot's PER + 1 ops (<= 5) follow slot gi
+    __builtin_amdgcn_s_barrier();
+    // the previous tile's epilogue, one chunk per k-tile (nk >= NCHUNK), beside this tile's MFMAs
+    if (ptile >= 0 && kt < NCHUNK) chunk(ptile, kt);
+    if (gi + S - 1 < total) issue(gi + S - 1);
+    const char* Ab = lds + (gi % S) * STAGE + (wm * WTM + lr) * RB + so;
+    const char* Bb = lds + (gi % S) * STAGE + A_BYTES + (wn * WTN + lr) * RB + so;
+    bf16x8 bfv[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * RB);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * RB);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[j], acc[i][j], 0, 0, 0);
+    }
+    if (++kt == nk) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every parked chunk read
+      // park: LayerNorm fold, bias, round to bf16 (the vector epilogue's order: rstd (acc - mean colsum) + bias);
+      // the epilogue operands landed with this tile's first k-tile, long waited for
+      const char* eb = epi + (lt & 1) * EPI;
+      float csum[TN], bia[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WTN + j * 16 + lr;
+        csum[j] = *reinterpret_cast<const float*>(eb + 2048 + col * 4);
+        bia[j] = *reinterpret_cast<const float*>(eb + 2560 + col * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pr0 = wm * WTM + i * 16 + lq * 4;
+        float2 lnr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lnr[r] = *reinterpret_cast<const float2*>(eb + (pr0 + r) * 8);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            float v = acc[i][j][r];
+            if (a.ln_rows) v = lnr[r].y * __builtin_fmaf(-lnr[r].x, csum[j], v);
+            if (a.bias) v += bia[j];
+            *reinterpret_cast<bf16*>(park + (pr0 + r) * PROW + (wn * WTN + j * 16 + lr) * 2) = from_f32<bf16>(v);
+            acc[i][j][r] = 0.f;
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // parked before the next barrier
+      ptile = wgid + lt * nwg;
+      ++lt;
+      kt = 0;
+    }
+  }
+  if (ptile >= 0) {
+    __builtin_amdgcn_s_barrier();
+    for (int c = 0; c < NCHUNK; ++c) chunk(ptile, c);
+  }
+}
+
+// persistent short-K linear (rdeic_set_conv_option(12, v)): 0 off (default), 1 where no tile is named
+// (rdeic_conv2d, tile -1), 2 also over a named tile 20..39 (the tile table's picks); tile 40 names it explicitly.
+// Off: measured slower than the LDS-DMA tiles on every transformer projection (r05, tools/lp_bench.py,
+// profiles/r05_lpersist.jsonl: 262 vs 252 us on the 65536 x 320 -> 2560 GEGLU, 1.4-1.7x slower at K >= 640).
+// Its k-loop alone (no output) took 225 us there: a 3-slot ring of 32-deep k-tiles keeps ~1k MFMA cycles in
+// flight per SIMD, under the L2 -> LDS latency, and the park buffer leaves no LDS for a deeper ring.
+int g_lpersist = 0;
+
+// eligibility: bf16 1x1 stride-1 projection, one input segment, K a multiple of 32, no residual / emb / act /
+// GroupNorm (input or statistics), output plain (mode 0, 16-byte rows) or GEGLU (mode 2)
+bool lp_ok(const rdeic_conv_desc* d, const ConvArgs& a, unsigned& b0, unsigned& bw, unsigned& bo) {
+  if (d->dtype != 1 || d->kh != 1 || d->kw != 1 || d->stride != 1 || d->pad_t || d->pad_l || d->up2 ||
+      d->c1 || a.batch > 1 || d->gn_ab || d->gn_part || d->res || d->emb || d->act || d->out_f32)
+    return false;
+  if (d->out_mode == 2) {
+    if (d->out_ld % 4 || ((uintptr_t)d->out) % 8) return false;
+  } else if (d->out_mode != 0 || d->out_ld % 8 || ((uintptr_t)d->out) % 16) {
+    return false;
+  }
+  if (d->c0 % lp::KB || d->c0 < 8 * lp::KB || d->ld0 % 8 || ((uintptr_t)d->in0) % 16 || d->cout % 8 || d->wld % 64)
+    return false;
+  if (a.M < 2048) return false;
+  const long e0 = ((long)(a.M - 1) * d->ld0 + d->c0) * 2, ew = (long)d->cout * d->wld * 2;
+  const long eo = ((long)(a.M - 1) * d->out_ld + (d->out_mode == 2 ? d->cout / 2 : d->cout)) * 2;
+  if (e0 >= (1l << 31) || ew >= (1l << 31) || eo >= (1l << 31)) return false;
+  b0 = (unsigned)e0;
+  bw = (unsigned)ew;
+  bo = (unsigned)eo;
+  return true;
+}
+
+int launch_lpersist(const ConvArgs& a, unsigned b0, unsigned bw, unsigned bo, hipStream_t s) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  const int tn = cdiv(a.cout, lp::BN);
+  const int ntiles = cdiv(a.M, lp::BM) * tn;
+  const int blocks = ntiles < cus ? ntiles : cus;
+  rdeic_count_launch(RDEIC_COUNT_LPERSIST);
+  if (a.out_mode == 2)
+    hipLaunchKernelGGL(linear_persist_kernel<true>, dim3(blocks), dim3(lp::NT), lp::LDS, s, a, tn, ntiles, b0, bw, bo);
+  else
+    hipLaunchKernelGGL(linear_persist_kernel<false>, dim3(blocks), dim3(lp::NT), lp::LDS, s, a, tn, ntiles, b0, bw, bo);
+  return launch_status();
+}
+
 int g_halo256 = 0;
 
 int g_halo8 = 1;  // the 8-row halo conv where it applies (rdeic_set_conv_option(9, v))
@@ -2594,6 +2862,10 @@ static int conv2d_run(const rdeic_conv_desc* d, void* stream, bool* fused) {
   float* const part = a.gn_part;
   a.gn_part = nullptr;  // statistics fuse into the LDS-DMA (dma_grouped reads d) and big-tile register paths
   hipStream_t s = (hipStream_t)stream;
+  {
+    unsigned lb0 = 0, lbw = 0, lbo = 0;
+    if (vec && g_lpersist && lp_ok(d, a, lb0, lbw, lbo)) return launch_lpersist(a, lb0, lbw, lbo, s);
+  }
   if (d->out_mode == 2) {  // fused GEGLU exists in the LDS-DMA kernel's vector epilogue only
     const int rc2 = vec ? dma_grouped(d, -1, 1, nullptr, s) : -1;
     return rc2 == -1 ? RDEIC_EINVAL : rc2;
@@ -2641,6 +2913,11 @@ static int conv2d_tile_run(const rdeic_conv_desc* d, int32_t tile, void* stream,
   bool vec = false;
   const int rc = make_args(d, a, vec);
   if (rc != RDEIC_OK) return rc;
+  {  // the persistent short-K linear takes its shapes whatever the table's tile (tile 40 = it, when eligible)
+    unsigned lb0 = 0, lbw = 0, lbo = 0;
+    if (vec && (tile == 40 || (tile < 20 && g_lpersist) || g_lpersist == 2) && lp_ok(d, a, lb0, lbw, lbo))
+      return launch_lpersist(a, lb0, lbw, lbo, (hipStream_t)stream);
+  }
   if (d->out_mode == 2) {
     const int rc2 = vec ? dma_grouped(d, tile >= 20 ? tile : -1, 1, nullptr, (hipStream_t)stream) : -1;
     return rc2 == -1 ? RDEIC_EINVAL : rc2;
@@ -2815,5 +3092,6 @@ extern "C" int rdeic_set_conv_option(int32_t key, int32_t value) {
   if (key == 9) { int prev = g_halo8; g_halo8 = value; return prev; }
   if (key == 10) { int prev = g_halo256; g_halo256 = value; return prev; }
   if (key == 11) { int prev = g_sk_fold; g_sk_fold = value; return prev; }
+  if (key == 12) { int prev = g_lpersist; g_lpersist = value; return prev; }
   return RDEIC_EINVAL;
 }

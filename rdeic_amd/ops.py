@@ -530,8 +530,8 @@ HALO_MAX_C = 512
 
 
 # launch counters of the library (rdeic_launch_count, RDEIC_COUNT_* in include/rdeic_hip.h)
-COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED, COUNT_SPLITK, COUNT_HALO256 = \
-    0, 1, 2, 3, 4, 5, 6
+COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED, COUNT_SPLITK, COUNT_HALO256, \
+    COUNT_LPERSIST = 0, 1, 2, 3, 4, 5, 6, 7
 
 
 def launch_count(kind: int) -> int:
