@@ -1357,6 +1357,8 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
 //   37 128x160/4 S2 and 38 64x160/4 S2 (N = 320 layers: two N tiles, no padded columns),
 //   39 256x128/8 S3 with 32-deep k-tiles (72 KB: two blocks per CU, so one block's epilogue overlaps the
 //   other's k-loop; for the short-K transformer linears, r05)
+// (r05: 256x256/16 S4 with 32-deep k-tiles, tile 32's 128 KB as four slots, ran 2-5% slower than tile 32 on
+//  every linear and 3x3 conv shape: profiles/r05_tile_s4_kb32.jsonl)
 // (r04: 16-wave S3 / S4 rings for the short-K linears, 256x128 S3, 128x256 S3, 128x128 S4, were
 //  slower than these S2 tiles on every transformer linear: profiles/r04_linear_tiles.jsonl)
 // Measured (tools/dma_bench.py, one MI355X): 32 is best where a 256x256 grid fills the chip

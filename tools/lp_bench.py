@@ -42,7 +42,9 @@ def main():
             p = st.conv_geglu("l0") if geglu else st.conv("l0")
         res = {"shape": [rows, cin, cout], "geglu": geglu, "ln": ln}
         for opt in OPTS:
-            prev = ops.set_conv_option(12, opt)
+            # opt < 20: option 12 (persistent linear) value; opt >= 20: that LDS-DMA tile forced, option 12 off
+            prev = ops.set_conv_option(12, opt if opt < 20 else 0)
+            ops.FORCE_TILE = opt if opt >= 20 else None
             try:
                 y = ops.linear(x, p, geglu=geglu, images=1, ln_rows=ms)
                 best = 1e9
@@ -56,6 +58,7 @@ def main():
                     best = min(best, e0.elapsed_time(e1) / 10 * 1e3)
             finally:
                 ops.set_conv_option(12, prev)
+                ops.FORCE_TILE = None
             res[f"us_opt{opt}"] = round(best, 1)
             res[f"tflops_opt{opt}"] = round(2.0 * rows * cin * cout / (best * 1e-6) / 1e12, 1)
         print(json.dumps(res), flush=True)
