@@ -1357,6 +1357,10 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
 //   37 128x160/4 S2 and 38 64x160/4 S2 (N = 320 layers: two N tiles, no padded columns),
 //   39 256x128/8 S3 with 32-deep k-tiles (72 KB: two blocks per CU, so one block's epilogue overlaps the
 //   other's k-loop; for the short-K transformer linears, r05)
+// (r05: 128x320/8 S2, 64 x 80 per wave, the whole N = 320 in one tile so the 64^2 3x3 convs gather their im2col
+//  A rows once instead of once per 160-wide N tile of tile 37: equal to tile 37 there (778 / 776, 1049 / 1031,
+//  1120 / 1120 TF), slower on the 1280-channel levels: profiles/r05_tile_128x320.jsonl; the 4.9x PMC
+//  re-read of tile 37 is absorbed by the L2 / MALL, not a bound)
 // (r05: 256x256/16 S4 with 32-deep k-tiles, tile 32's 128 KB as four slots, ran 2-5% slower than tile 32 on
 //  every linear and 3x3 conv shape: profiles/r05_tile_s4_kb32.jsonl)
 // (r04: 16-wave S3 / S4 rings for the short-K linears, 256x128 S3, 128x256 S3, 128x128 S4, were
