@@ -21,6 +21,10 @@ SHAPES = [  # name, B, heads, lq, lk, dh, kv_bcast
 ]
 
 
+# rdeic_set_conv_option(1, mode) values timed for dh = 64 (argv[1], comma-separated; default 0,1,2)
+MODES = tuple(int(v) for v in sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 1, 2)
+
+
 def bench(fn, reps):
     torch.cuda.synchronize()
     t = time.perf_counter()
@@ -45,7 +49,7 @@ def main():
             return o.clone()
         res = {"name": name}
         outs = {}
-        modes = (0, 1, 2) if dh == 64 else (2,)
+        modes = MODES if dh == 64 else (2,)
         for mode in modes:
             ops.set_conv_option(1, mode)
             outs[mode] = fn()
