@@ -1541,9 +1541,9 @@ __device__ __forceinline__ void halo_res_dma(__amdgpu_buffer_rsrc_t rsr, char* d
 // The halo convs' epilogue for bf16 outputs without emb / activation (every VAE ResnetBlock conv):
 // out = (acc + bias) + residual, rounded to bf16, in four passes (one 16-row fragment per wave row, NW x 8
 // tile rows). Per pass: the accumulators of fragment row p are parked in LDS (park); the residual rows of
-// the pass are already in LDS (r0 / r1 alternate; LDS-DMA issued one pass ahead, so its latency overlaps
-// the previous pass instead of stalling every chunk; pass 0's is issued by the caller during its last
-// taps); each thread keeps the bias of its 8 channels in registers and handles 2 chunks (16-byte LDS reads,
+// the pass are already in LDS (r0 / r1 alternate; LDS-DMA issued one pass ahead, right after the barrier that
+// frees its buffer, so its latency overlaps the previous pass and this pass's park; pass 0's is issued by the
+// caller during its last taps); each thread keeps the bias of its 8 channels in registers and handles 2 chunks (16-byte LDS reads,
 // residual read, one 16-byte store each). Arithmetic and rounding are epilogue_vec's, so outputs are
 // bit-identical to it. Fused GroupNorm statistics (a.gn_part) keep the canonical order: pass p is 16-row
 // group p of every 64-row block (one wave row), summed by a column scan of the stored values, and
@@ -1574,16 +1574,19 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     __syncthreads();  // p = 0: the main loop's LDS reads are done; else: the previous pass's readers are
+    // the next pass's residual into the buffer pass p - 1 read, as soon as its readers are past the barrier
+    // (before this pass's park: the park's time adds to its lead)
+    if (has_res && p + 1 < 4)
+      halo_res_dma<NW>(rsr, lds + ((p + 1) & 1 ? r1 : r0), base, W, a.res_ld, n0, wave, lane, p + 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j) L[(wm * 16 + lq * 4 + r) * SDW + wn * 64 + j * 16 + lr] = acc[p][j][r];
-    if (has_res) {  // this wave's residual pieces of pass p (younger: the 2 stores of pass p - 1)
-      if (p == 0) wait_vm<0>(); else wait_vm<2>();
+    if (has_res) {  // this wave's residual pieces of pass p; younger: the next pass's 2 pieces (p < 3) and the
+      // 2 stores of pass p - 1 (p > 0); at p = 0 every main-loop op is complete (its last wait drained them)
+      if (p == 0) wait_vm<2>(); else if (p < 3) wait_vm<4>(); else wait_vm<2>();
     }
     __syncthreads();
-    if (has_res && p + 1 < 4)  // the next pass's residual into the buffer pass p - 1 read
-      halo_res_dma<NW>(rsr, lds + ((p + 1) & 1 ? r1 : r0), base, W, a.res_ld, n0, wave, lane, p + 1);
     const char* R = lds + (p & 1 ? r1 : r0);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
