@@ -1548,7 +1548,7 @@ __device__ __forceinline__ void halo_res_dma(__amdgpu_buffer_rsrc_t rsr, char* d
 // bit-identical to it. Fused GroupNorm statistics (a.gn_part) keep the canonical order: pass p is 16-row
 // group p of every 64-row block (one wave row), summed by a column scan of the stored values, and
 // ((g0 + g1) + g2) + g3 at the end.
-template <int NW>
+template <int NW, bool RES>
 __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const ConvArgs& a, int n0, int wm, int wn,
                                               int tid, char* lds, int base, int W, int park, int r0, int r1,
                                               __amdgpu_buffer_rsrc_t rsr, int wave) {
@@ -1559,7 +1559,8 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
   const int lane = tid & 63;
   const int lr = lane & 15, lq = lane >> 4;
   float* const L = reinterpret_cast<float*>(lds + park);
-  const bool has_res = a.res != nullptr;
+  constexpr bool has_res = RES;  // a.res != nullptr, a compile-time split (no branch around the residual loads,
+                                 // whose vmcnt scoreboard the compiler would otherwise merge over both paths)
   const bool st = a.gn_part != nullptr;
   const int cc = tid & 15;  // this thread's 8 channels n0 + 8 cc (NT % 16 == 0: the same in every chunk)
   const int nn = n0 + cc * 8;
@@ -1571,23 +1572,36 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
     bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w; bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
   }
   float sg[4], qg[4];
+  // LDS-only barriers (__syncthreads() would also drain vmcnt(0): the previous pass's output stores and the
+  // next pass's residual loads). The residual of pass 0 is in LDS (r0, LDS-DMA'd by the caller during its
+  // last taps); passes 1-3 load theirs into registers one pass ahead (an LDS-DMA here would make the compiler
+  // drain vmcnt(0) before the next LDS read, i.e. wait out the prefetch at once).
+  auto bar = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto res_rows = [&](int p, uint4 (&dst)[2]) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pr = (tid >> 4) + (NT / 16) * k;
+      const long m = base + (pr >> 4) * W + p * 16 + (pr & 15);
+      // a buffer load through the residual's descriptor (a plain load here compiled to flat_load, which counts
+      // in lgkmcnt too, so every LDS barrier would wait for it)
+      typedef unsigned u4v __attribute__((ext_vector_type(4)));
+      const u4v r = __builtin_amdgcn_raw_buffer_load_b128(rsr, (unsigned)(m * a.res_ld + nn) * 2u, 0, 0);
+      dst[k] = uint4{r.x, r.y, r.z, r.w};
+    }
+  };
+  uint4 rbuf[2][2];  // [pass & 1][chunk]: pass p reads rbuf[p & 1], pass p + 1's rows load into the other
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    __syncthreads();  // p = 0: the main loop's LDS reads are done; else: the previous pass's readers are
-    // the next pass's residual into the buffer pass p - 1 read, as soon as its readers are past the barrier
-    // (before this pass's park: the park's time adds to its lead)
-    if (has_res && p + 1 < 4)
-      halo_res_dma<NW>(rsr, lds + ((p + 1) & 1 ? r1 : r0), base, W, a.res_ld, n0, wave, lane, p + 1);
+    bar();  // p = 0: the main loop's LDS reads are done; else: the previous pass's readers are
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j) L[(wm * 16 + lq * 4 + r) * SDW + wn * 64 + j * 16 + lr] = acc[p][j][r];
-    if (has_res) {  // this wave's residual pieces of pass p; younger: the next pass's 2 pieces (p < 3) and the
-      // 2 stores of pass p - 1 (p > 0); at p = 0 every main-loop op is complete (its last wait drained them)
-      if (p == 0) wait_vm<2>(); else if (p < 3) wait_vm<4>(); else wait_vm<2>();
-    }
-    __syncthreads();
-    const char* R = lds + (p & 1 ? r1 : r0);
+    if (has_res && p == 0) wait_vm<0>();  // this wave's pass-0 residual pieces (nothing else is in flight)
+    bar();
+    // consumed one pass later; pass 0 issues pass 1's after its LDS residual reads (the compiler drains
+    // vmcnt(0) before the first read of LDS-DMA'd data)
+    if (has_res && p > 0 && p + 1 < 4) res_rows(p + 1, rbuf[(p + 1) & 1]);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int pr = (tid >> 4) + (NT / 16) * k;  // pass row: wave row pr / 16, row p * 16 + pr % 16 of it
@@ -1598,7 +1612,9 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += bias[e];
       if (has_res) {
-        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + pr * 256 + cc * 16);
+        bf16x8 rv;
+        if (p == 0) rv = *reinterpret_cast<const bf16x8*>(lds + r0 + pr * 256 + cc * 16);
+        else *reinterpret_cast<uint4*>(&rv) = rbuf[p & 1][k];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
       }
@@ -1611,8 +1627,9 @@ __device__ __forceinline__ void halo_epilogue(const f32x4 (&acc)[4][4], const Co
         *reinterpret_cast<float4*>(L + pr * SDW + cc * 8 + 4) = make_float4((float)ov[4], (float)ov[5], (float)ov[6], (float)ov[7]);
       }
     }
+    if (has_res && p == 0) res_rows(1, rbuf[1]);
     if (st) {  // column scan: thread (wave row b, channel j), the 16 rows of group p, in row order
-      __syncthreads();
+      bar();
       const int b = tid >> 7, j = tid & 127;
       const float* col = L + (b * 16) * SDW + j;
       float y[16];
@@ -1833,12 +1850,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
   }
   HALO_STAMP(2);
-  if constexpr (FE)
-    halo_epilogue<NW>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(parity),
-                      res_off(parity, 0), res_off(parity, 1), rsr, wave);
-  else
+  if constexpr (FE) {
+    if (a.res)
+      halo_epilogue<NW, true>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(parity),
+                              res_off(parity, 0), res_off(parity, 1), rsr, wave);
+    else
+      halo_epilogue<NW, false>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(parity),
+                               res_off(parity, 0), res_off(parity, 1), rsr, wave);
+  } else {
     epilogue_vec<TR * TC, BN, 4, 2, NT, 2, Rows, false>(acc, a, 0, n0, wm, wn, lane, tid, lds,
                                                         Rows{(img * H + oy0) * W + ox0, W});
+  }
   HALO_STAMP(3);
 }
 
@@ -2111,8 +2133,12 @@ __global__ __launch_bounds__(1024) void conv3x3_halo8_kernel(ConvArgs a, int til
     }
   }
   HALO_STAMP(2);
-  halo_epilogue<NW>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(f), res_off(f, 0),
-                    res_off(f, 1), rsr, wave);
+  if (a.res)
+    halo_epilogue<NW, true>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(f), res_off(f, 0),
+                            res_off(f, 1), rsr, wave);
+  else
+    halo_epilogue<NW, false>(acc, a, n0, wm, wn, tid, lds, (img * H + oy0) * W + ox0, W, park_off(f), res_off(f, 0),
+                             res_off(f, 1), rsr, wave);
   HALO_STAMP(3);
 }
 
