@@ -14,7 +14,7 @@ CXXFLAGS := -O3 -fPIC -std=c++17 -Wall -pthread
 
 all: $(LIB) oracle
 
-$(BUILD)/%.hip.o: rdeic_amd/csrc/%.hip rdeic_amd/csrc/common.h rdeic_amd/csrc/prof.h include/rdeic_hip.h
+$(BUILD)/%.hip.o: rdeic_amd/csrc/%.hip rdeic_amd/csrc/common.h rdeic_amd/csrc/conv_common.h rdeic_amd/csrc/prof.h include/rdeic_hip.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -44,4 +44,4 @@ $(BUILD)/elementwise.hip.o $(BUILD)/entropy.hip.o: HIPFLAGS += -ffp-contract=off
 
 # conv kernels: no SLP vectorisation (packed-f32 VALU beside MFMAs is an anti-lever on gfx950,
 # MI355X_MICROARCH.md constants table; measured r04 on the halo conv: -1 to -2% time)
-$(BUILD)/conv_gemm.hip.o: HIPFLAGS += -fno-slp-vectorize
+$(BUILD)/conv_gemm.hip.o $(BUILD)/conv_dma.hip.o $(BUILD)/conv_halo.hip.o $(BUILD)/conv_edge.hip.o: HIPFLAGS += -fno-slp-vectorize

@@ -92,20 +92,17 @@ int rdeic_conv2d(const rdeic_conv_desc* d, void* stream);
  * prologue): 0 256x256/16 waves, 1 256x128/8, 2 128x256/8, 3 128x128/4, 4 64x128/4,
  * 6 256x128/16, 7 128x256/16, 8 128x128/8, 9 128x128/16, 10 64x128/8. LDS-DMA tiles (bf16, both
  * concat segments multiples of 64 channels; other shapes fall back to the register path):
- * 20 256x256/8, 21 256x128/8, 22 128x256/8, 23-24 128x128/4, 25 128x128/8, 26 64x128/4,
+ * 21 256x128/8, 22 128x256/8, 23-24 128x128/4, 25 128x128/8, 26 64x128/4,
  * 27 128x128/8, 28 256x128/8, 29 128x256/8, 30 64x128/4, 31 128x64/4, 32 256x256/16,
- * 33 256x128/16, 34 128x128/16, 35 512x128/16, 36 64x128/8, 37 128x160/4, 38 64x160/4,
- * 39 256x128/8 with 32-deep k-tiles (two blocks per CU; ring depths in conv_gemm.hip). -1 = heuristic.
+ * 33 256x128/16, 34 128x128/16, 35 512x128/16, 36 64x128/8, 37 128x160/4, 38 64x160/4
+ * (ring depths in conv_dma.hip). -1 = heuristic.
  * All tiles give
  * bit-identical results (same k order, same MFMA), so a caller may autotune. */
 int rdeic_conv2d_tile(const rdeic_conv_desc* d, int32_t tile, void* stream);
 /* Split-K variant for small-M / large-K layers (the UNet's 8x8 and 16x16 levels): `splits`
  * k-ranges accumulate into the caller's workspace, then a reduction sums them in split order
- * (deterministic) and applies bias / emb / act / residual. ws: 4096 int32 tile counters that must be
- * zero (they are left zero), then >= splits * n*ho*wo * cout fp32 partials (ws_floats counts both). With
- * rdeic_set_conv_option(11, 1) the LDS-DMA path folds the reduction, and the output's GroupNorm
- * statistics (gn_part), into the producing launch (the last split of each output tile reduces it).
- * bf16 only, no GN prologue, out_mode 0, batch 1, cout % 8 == 0. Not bit-identical to
+ * (deterministic) and applies bias / emb / act / residual. ws: >= splits * n*ho*wo * cout fp32 partials.
+ * bf16 or fp32, no GN prologue, out_mode 0, batch 1, cout % 8 == 0. Not bit-identical to
  * rdeic_conv2d (different k grouping): not for the entropy-model nets. */
 int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, size_t ws_floats, void* stream);
 /* 2 (default): bf16 convs without a GN prologue pick among the big register-staged tiles
@@ -115,7 +112,6 @@ int rdeic_conv2d_splitk(const rdeic_conv_desc* d, int32_t splits, float* ws, siz
 int rdeic_set_conv_path(int32_t path);
 /* Tuning switches (process-wide). key 0: LDS-staged vector epilogue on (1, default) / off (0);
  * key 1: transposed head-dim-64 attention kernel on (1, default) / off (0);
- * key 2: two-deep register prefetch in the register-staged conv path (0 default, 1 on);
  * key 3: XOR-swizzled 128-byte LDS rows on the <= 8-wave conv tiles (1 default) / padded rows (0);
  * key 4: force the big-tile candidate (0 256x256, 1 256x128, 2 128x256, 3 128x128, 4 64x128,
  *        5 128x64; -1 = automatic choice, default) — tuning only;
@@ -128,17 +124,9 @@ int rdeic_set_conv_path(int32_t path);
  * key 9: the halo conv's 8-row form (one 1024-thread block per CU, 8-slot weight ring) where the
  *        output height is a multiple of 8 and the epilogue is bf16 without emb / activation: 1 on
  *        (default), 0 the 4-row form everywhere (bit-identical outputs);
- * key 10: the halo conv's 256-channel form (4 x 64 pixels x 256 channels per 1024-thread block) where
- *        cout % 256 == 0 and the epilogue is bf16 without emb / activation: 1 on, 0 off (default: it
- *        measured 2-3% slower than the 8-row form); bit-identical outputs either way;
- * key 11: split-K reduction (and GroupNorm statistics) folded into the producing launch (1) / a separate
- *        reduce (and statistics) launch (0, default: the fold measured slower); bit-identical either way;
- * key 12: the persistent short-K linear (bf16 1x1 projections, K a multiple of 32 and >= 256, output plain
- *        or GEGLU, LayerNorm fold / bias, no residual / emb / activation / GroupNorm, >= 2048 rows): one
- *        block per CU walks 256 x 128 tiles and runs each tile's epilogue beside the next tile's MFMAs.
- *        0 off (default: measured slower, its 3-slot ring of 32-deep k-tiles is latency-bound), 1 where
- *        no tile is named, 2 also over a named tile 20..39; tile 40 of rdeic_conv2d_tile names it.
- *        Bit-identical to the LDS-DMA tiles.
+ * key 10: the VAE edge convs (conv_edge.hip): conv_in from 8 input channels on direct-load MFMA fragments
+ *        (bit-identical to the register tile) and norm -> SiLU -> conv to <= 16 channels (fp32 rounding of the
+ *        sums differs from the tiny-cout kernel): 1 on (default), 0 off.
  * Returns the previous value, or -22 for an unknown key. Results are bit-identical either way
  * (keys 0-5; 6 and 8 change fp32 rounding only). */
 int rdeic_set_conv_option(int32_t key, int32_t value);
@@ -352,9 +340,8 @@ int rdeic_prof_start(int32_t capacity, int32_t every);
 #define RDEIC_COUNT_HALO_SMALL 3   /* the small-image halo conv (UNet / control ResBlocks) */
 #define RDEIC_COUNT_LN_FUSED 4     /* rdeic_layernorm_rowstats (LayerNorm folded into the next linear) */
 #define RDEIC_COUNT_SPLITK 5       /* rdeic_conv2d_splitk launches that ran split (partial pass + reduce) */
-#define RDEIC_COUNT_HALO256 6      /* conv3x3_halo256_kernel (the 256-channel halo conv, cout % 256 == 0) */
-#define RDEIC_COUNT_LPERSIST 7     /* linear_persist_kernel (the persistent short-K linear, option 12) */
-#define RDEIC_COUNT_KINDS 8
+#define RDEIC_COUNT_EDGE 6         /* the VAE edge convs (conv_edge.hip: conv_in from 8 channels, norm -> SiLU -> conv to <= 16) */
+#define RDEIC_COUNT_KINDS 8        /* 7: unused */
 int64_t rdeic_launch_count(int32_t kind);
 /* Per-row LayerNorm statistics (attention.py:273-285, torch.nn.LayerNorm: biased variance, eps) of
  * bf16 rows x[rows][c] (pixel stride ld): ms[2 r] = mean, ms[2 r + 1] = 1 / sqrt(var + eps), two-pass

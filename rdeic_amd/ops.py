@@ -103,7 +103,8 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     ln_rows: [M, 2] fp32 (mean, rstd) of the raw input rows from layer_norm_rowstats, with p packed by
     ParamStore.conv_ln: the output is linear(LayerNorm(x)) (the LayerNorm folded into the GEMM)."""
     if gn is not None and _gn_materialize(x, x2, p) and not _halo_eligible(x, x2, p, up2, pad_t, pad_l, out_hw,
-                                                                           geglu or pixel_shuffle, out):
+                                                                           geglu or pixel_shuffle, out) \
+            and not _edge_narrow_eligible(x, x2, p, up2, pad_t, pad_l, out_hw, geglu or pixel_shuffle or emb is not None):
         # the big-tile conv path has no GroupNorm prologue (it is VALU-bound there): materialise the
         # normalised (concatenated) input once with the vectorised, HBM-rate apply kernel instead
         xin = torch.empty(x.shape[:3] + (p.cin,), dtype=x.dtype, device=x.device)
@@ -208,7 +209,7 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
 
     tag = ("conv", flops, (n, h, w, c0, c1, p.cout, p.kh, p.stride, gn is not None, int(up2), d.out_mode))
     if splits > 1:
-        ws = _splitk_workspace(SPLITK_COUNTERS + splits * n * ho * wo * p.cout, x.device)
+        ws = _splitk_workspace(splits * n * ho * wo * p.cout, x.device)
         _launch(tag, "rdeic_conv2d_splitk", C.byref(d), splits, ws.data_ptr(), ws.numel(), stream_ptr())
     elif tile >= 0:
         _launch(tag, "rdeic_conv2d_tile", C.byref(d), tile, stream_ptr())
@@ -245,14 +246,14 @@ def _gn_part_of(t: Optional[torch.Tensor], hw: int):
 # (conv_tiles.json, measured once on an MI355X by tools/tune_tiles.py): the same kernel runs for a
 # given shape in every process and on every box. Shapes missing from the table use the library's
 # built-in heuristic (tile -1). AUTOTUNE (tuning runs only) times the candidates for missing shapes.
-# Layers whose channel segments are multiples of 64 run on the LDS-DMA kernel (tile ids 20..39,
+# Layers whose channel segments are multiples of 64 run on the LDS-DMA kernel (tile ids 21..38,
 # rdeic_hip.h); the others on the register-staged tiles (0..10).
 AUTOTUNE = False
 FORCE_TILE: Optional[int] = None  # tests / tools: run every eligible conv on this tile id
 GEGLU_FUSED = True  # bf16 transformer FF: GEGLU in the projection's epilogue (conv out_mode 2)
 TILE_CANDIDATES = (0, 1, 3, 4, 6, 8, 10)
-DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31, 35, 36, 37, 38, 39)
-ALL_TILES = (0, 1, 2, 3, 4, 6, 7, 8, 9, 10) + tuple(range(20, 40))
+DMA_TILE_CANDIDATES = (25, 32, 34, 26, 30, 33, 24, 31, 35, 36, 37, 38)
+ALL_TILES = (0, 1, 2, 3, 4, 6, 7, 8, 9, 10) + tuple(range(21, 39))
 # RDEIC_TILE_TABLE: another table file (same-box A/B of tile tables, tools/table_ab.sh)
 TILE_TABLE_PATH = os.environ.get("RDEIC_TILE_TABLE") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                      "conv_tiles.json")
@@ -396,20 +397,14 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
 _SPLITK_KEEP: list = []  # every workspace ever handed out: recorded launch plans hold their pointers
 
 
-# rdeic_conv2d_splitk's workspace starts with this many int32 tile counters (zero; the folded reduction
-# leaves them zero), then the fp32 partial slabs
-SPLITK_COUNTERS = 4096
-
-
 def _splitk_workspace(n: int, device) -> torch.Tensor:
     """Split-K partial-sum scratch, one per (device, stream): concurrent codec sessions (one per
-    stream) must not share it (nor its tile counters). A grown workspace replaces the old one for new
+    stream) must not share it. A grown workspace replaces the old one for new
     launches, but the old one stays allocated (plans recorded earlier still point at it)."""
     key = (str(device), stream_ptr())
     buf = _SPLITK_WS.get(key)
     if buf is None or buf.numel() < n:
         buf = torch.empty(n, dtype=torch.float32, device=device)
-        buf[:SPLITK_COUNTERS].zero_()
         _SPLITK_WS[key] = buf
         _SPLITK_KEEP.append(buf)
     return buf
@@ -513,11 +508,13 @@ def set_conv_path(path: int) -> int:
 
 
 def set_conv_option(key: int, value: int) -> int:
-    """rdeic_set_conv_option: key 0 vectorised epilogue, 1 dh=64 attention kernel, 2 two-deep prefetch."""
+    """rdeic_set_conv_option (include/rdeic_hip.h): 0 vector epilogue, 1 dh=64 attention kernel, 3 swizzle,
+    4 forced register tile, 5 LDS-DMA path, 6 halo conv, 8 d=512 attention form, 9 8-row halo conv, 10 VAE edge
+    convs."""
     return int(_lib.load().rdeic_set_conv_option(int(key), int(value)))
 
 
-# 3x3 halo conv (rdeic_amd/csrc/conv_gemm.hip, conv3x3_halo_kernel): a conv whose input is a
+# 3x3 halo conv (rdeic_amd/csrc/conv_halo.hip, conv3x3_halo8_kernel / conv3x3_halo_kernel): a conv whose input is a
 # GroupNorm (+ SiLU) of a single 32-channel-aligned NHWC tensor and whose output tiles as 4 x 64 pixel
 # blocks x 128 channels takes the raw input and applies the affine once per element in LDS, instead
 # of materialising the normalised tensor (rdeic_set_conv_option(6, .): 0 off, 1 GroupNorm inputs, 2 all).
@@ -530,8 +527,8 @@ HALO_MAX_C = 512
 
 
 # launch counters of the library (rdeic_launch_count, RDEIC_COUNT_* in include/rdeic_hip.h)
-COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED, COUNT_SPLITK, COUNT_HALO256, \
-    COUNT_LPERSIST = 0, 1, 2, 3, 4, 5, 6, 7
+COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED, COUNT_SPLITK, COUNT_EDGE = \
+    0, 1, 2, 3, 4, 5, 6
 
 
 def launch_count(kind: int) -> int:
@@ -566,6 +563,34 @@ def _halo_eligible(x, x2, p: "ConvParams", up2, pad_t, pad_l, out_hw, special, o
     if out is not None and (pix_ld(out) % 8 or out.data_ptr() % 16):
         return False
     return True
+
+
+# The VAE edge convs (rdeic_amd/csrc/conv_edge.hip, rdeic_set_conv_option(10, .)): conv_in from 8 channels on
+# direct-load MFMA fragments, and norm -> SiLU -> 3x3 conv to <= 16 channels (the decoder's conv_out) with the
+# GroupNorm applied once per element in LDS instead of materialised (one read of the input instead of read + write
+# + read).
+EDGE_CONV = 1
+
+
+def set_edge_conv(mode: int) -> int:
+    global EDGE_CONV
+    prev = EDGE_CONV
+    EDGE_CONV = int(mode)
+    _lib.load().rdeic_set_conv_option(10, EDGE_CONV)
+    return prev
+
+
+def _edge_narrow_eligible(x, x2, p: "ConvParams", up2, pad_t, pad_l, out_hw, special) -> bool:
+    """Mirror of the library's launch_edge rule for the GroupNorm-input narrow conv."""
+    if not EDGE_CONV or x.dtype != torch.bfloat16 or x2 is not None or up2 or special:
+        return False
+    if p.kh != 3 or p.kw != 3 or p.stride != 1 or p.pad != 1 or (pad_t not in (None, 1)) or (pad_l not in (None, 1)):
+        return False
+    n, h, w, c = x.shape
+    if out_hw is not None and tuple(out_hw) != (h, w):
+        return False
+    return p.cout <= 16 and c % 32 == 0 and c <= 512 and h % 16 == 0 and w % 64 == 0 and x.stride(2) % 8 == 0 \
+        and x.data_ptr() % 16 == 0
 
 
 def _gn_materialize(x: torch.Tensor, x2: Optional[torch.Tensor], p: ConvParams) -> bool:

@@ -143,58 +143,3 @@ def test_halo8_bit_identical_to_halo4(gpu, n, h, w, cin, cout, silu):
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.parametrize("n,h,w,cin,cout,silu,use_res", [(2, 16, 128, 128, 256, True, True),
-                                                         (1, 8, 64, 512, 512, True, True),
-                                                         (2, 12, 64, 96, 256, False, True),
-                                                         (1, 16, 192, 256, 512, True, False),
-                                                         (2, 4, 64, 32, 256, True, True)])
-def test_halo256_bit_identical_to_halo8_and_halo4(gpu, n, h, w, cin, cout, silu, use_res):
-    """The 256-channel halo conv (rdeic_set_conv_option(10, 1)) keeps the 4- and 8-row kernels' MFMA order
-    and epilogue arithmetic: outputs and fused statistics are bit-identical to both (h = 12 / 4: the 8-row
-    form does not apply, the 4-row form is the reference), with and without the residual, for channel-block
-    counts whose last tap leaves the epilogue's residual buffer at either ring position."""
-    from rdeic_amd import ops
-    torch.manual_seed(h * cin + cout + 1)
-    x = (torch.randn(n, h, w, cin, device="cuda") * 1.3 - 0.2).to(torch.bfloat16)
-    _, _, p = _params(cin, cout, seed=cin * 5 + cout)
-    ab = _gn_ab(x, 32, seed=13)
-    res = torch.randn(n, h, w, cout, device="cuda").to(torch.bfloat16) if use_res else None
-    outs = []
-    for o10, o9 in ((1, 1), (0, 1), (0, 0)):
-        p10, p9 = ops.set_conv_option(10, o10), ops.set_conv_option(9, o9)
-        try:
-            c0 = ops.launch_count(ops.COUNT_HALO256)
-            y = _run(x, p, ab, silu=silu, res=res, stats=True)
-            assert (ops.launch_count(ops.COUNT_HALO256) > c0) == bool(o10)
-            gamma, beta = torch.ones(cout, device="cuda"), torch.zeros(cout, device="cuda")
-            outs.append((y, ops.group_norm_ab(y, gamma, beta, 32, 1e-6)))
-        finally:
-            ops.set_conv_option(10, p10)
-            ops.set_conv_option(9, p9)
-    torch.cuda.synchronize()
-    for y, st in outs[1:]:
-        assert torch.equal(outs[0][0], y)
-        assert torch.equal(outs[0][1], st)
-
-
-def test_halo256_plain_conv_and_batch_invariance(gpu):
-    """No GroupNorm (halo mode 2) through the 256-channel form, against the 4-row form bit for bit, and
-    batch invariance of the 256-channel form."""
-    from rdeic_amd import ops
-    x = torch.randn(3, 8, 128, 128, device="cuda").to(torch.bfloat16)
-    _, _, p = _params(128, 256, seed=21)
-    prev = ops.set_halo_conv(2)
-    try:
-        y = ops.conv2d(x, p)
-        y1 = ops.conv2d(x[2:3].contiguous(), p)
-        p10 = ops.set_conv_option(10, 0)
-        try:
-            y4 = ops.conv2d(x, p)
-        finally:
-            ops.set_conv_option(10, p10)
-    finally:
-        ops.set_halo_conv(prev)
-    assert torch.equal(y[2:3], y1)
-    assert torch.equal(y, y4)

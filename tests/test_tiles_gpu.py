@@ -4,7 +4,7 @@ The encoder and decoder entropy models must compute identical mu / sigma (SURVEY
 hazard 8), and the per-shape tile table (rdeic_amd/conv_tiles.json) may pick any tile. This runs a
 small bf16 codec (VAE encoder, entropy nets, 20 checkerboard stages, relay UNet + control, VAE
 decoder) with ops.conv2d wrapped: at the first call of each distinct layer shape, the same conv is
-re-run with every tile id (register tiles 0-10, LDS-DMA tiles 20-39) and with the built-in
+re-run with every tile id (register tiles 0-10, LDS-DMA tiles 21-38) and with the built-in
 heuristic, and each result must equal the table's output bit for bit — and so must the GroupNorm
 statistics fused into the epilogue of the convs that produce them (or computed by the stand-alone
 fallback where a tile cannot fuse them)."""

@@ -1,5 +1,5 @@
 // Diagnostic: where does an LDS-DMA conv tile (conv_dma_kernel) spend its time on a transformer linear?
-// Compiles conv_gemm.hip with per-block shader-clock stamps (RDEIC_HALO_STAMPS: entry, prologue DMA issued,
+// Compiles the conv sources (conv_gemm / conv_dma / conv_halo.hip) with per-block shader-clock stamps (RDEIC_HALO_STAMPS: entry, prologue DMA issued,
 // k-loop end, epilogue end) and runs one 1x1 "conv" over M token rows through the library's own dispatch
 // (rdeic_conv2d_tile), optionally with the fused GEGLU epilogue and a residual. Prints the event-timed
 // launch and the per-block phase split (medians), plus the k-loop cycles per k-tile.
@@ -9,6 +9,8 @@
 //   tools/dma_stamps M K N TILE [geglu res]
 #define RDEIC_HALO_STAMPS 1
 #include "../rdeic_amd/csrc/conv_gemm.hip"
+#include "../rdeic_amd/csrc/conv_dma.hip"
+#include "../rdeic_amd/csrc/conv_halo.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -37,14 +39,14 @@ static double pct(std::vector<double> v, double q) {
   return v.empty() ? 0 : v[(size_t)(q * (v.size() - 1))];
 }
 
-static const int BMS[] = {256, 256, 128, 128, 128, 128, 64, 128, 256, 128, 64, 128, 256, 256, 128, 512, 64, 128, 64, 256};
-static const int BNS[] = {256, 128, 256, 128, 128, 128, 128, 128, 128, 256, 128, 64, 256, 128, 128, 128, 128, 160, 160, 128};
+static const int BMS[] = {256, 128, 128, 128, 128, 64, 128, 256, 128, 64, 128, 256, 256, 128, 512, 64, 128, 64};  // tiles 21..38
+static const int BNS[] = {128, 256, 128, 128, 128, 128, 128, 128, 256, 128, 64, 256, 128, 128, 128, 128, 160, 160};
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 65536, K = argc > 2 ? atoi(argv[2]) : 320, N = argc > 3 ? atoi(argv[3]) : 2560;
   const int tile = argc > 4 ? atoi(argv[4]) : 32;
   const int geglu = argc > 5 ? atoi(argv[5]) : 0, use_res = argc > 6 ? atoi(argv[6]) : 0;
-  if (tile < 20 || tile > 39) { fprintf(stderr, "tile 20..39\n"); return 1; }
+  if (tile < 21 || tile > 38) { fprintf(stderr, "tile 21..38\n"); return 1; }
   const int wld = (K + 63) / 64 * 64;
   const int NO = geglu ? N / 2 : N;
   bf16 *x, *wt, *res = nullptr, *out;
@@ -58,7 +60,7 @@ int main(int argc, char** argv) {
   fill_bf16_k<<<4096, 256>>>(x, (long)M * K, 1, 2.f, 0.f);
   fill_bf16_k<<<1024, 256>>>(wt, (long)N * wld, 2, 0.1f, 0.f);
   if (use_res) fill_bf16_k<<<4096, 256>>>(res, (long)M * NO, 3, 1.f, 0.f);
-  const int bm = BMS[tile - 20], bn = BNS[tile - 20];
+  const int bm = BMS[tile - 21], bn = BNS[tile - 21];
   const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   unsigned long long* st;
   CK(hipMalloc(&st, tiles * 8 * 8));
@@ -100,7 +102,7 @@ int main(int argc, char** argv) {
     epi.push_back((double)(q[3] - q[2]));
     tot.push_back((double)(q[3] - q[0]));
   }
-  const int nk = wld / (tile == 39 ? 32 : 64);
+  const int nk = wld / 64;
   printf("{\"shape\": [%d, %d, %d], \"tile\": %d, \"bm\": %d, \"bn\": %d, \"geglu\": %d, \"res\": %d, \"us\": %.2f, "
          "\"tflops\": %.1f, \"tiles\": %ld, \"span_cycles\": %.0f, \"cycles\": {\"issue_med\": %.0f, \"kloop_med\": %.0f, "
          "\"kloop_p90\": %.0f, \"kloop_per_ktile\": %.0f, \"epilogue_med\": %.0f, \"epilogue_p90\": %.0f, "

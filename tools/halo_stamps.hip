@@ -1,4 +1,4 @@
-// Diagnostic: where does conv3x3_halo_kernel spend its time? Compiles conv_gemm.hip with per-block
+// Diagnostic: where does conv3x3_halo_kernel spend its time? Compiles the conv sources (conv_gemm / conv_dma / conv_halo.hip) with per-block
 // shader-clock stamps (RDEIC_HALO_STAMPS: kernel entry, main-loop start, main-loop end, epilogue end)
 // and runs the halo conv on one layer shape with random operands, through the library's own dispatch
 // (rdeic_conv2d). Prints the event-timed launch and the per-block phase split.
@@ -8,6 +8,8 @@
 //   tools/halo_stamps N H W C COUT [res stats]
 #define RDEIC_HALO_STAMPS 1
 #include "../rdeic_amd/csrc/conv_gemm.hip"
+#include "../rdeic_amd/csrc/conv_dma.hip"
+#include "../rdeic_amd/csrc/conv_halo.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -67,12 +69,9 @@ int main(int argc, char** argv) {
   fill_f32_k<<<64, 256>>>(ab, (long)N * C * 2, 5, 1.f, 0.5f);
   // HALO4=1 in the environment: the 4-row kernel everywhere (option 9 off)
   const int h8 = getenv("HALO4") && atoi(getenv("HALO4")) ? 0 : 1;
-  // H256=1: the 256-channel form (4 rows, option 10) where cout % 256 == 0
-  const int h256 = getenv("H256") && atoi(getenv("H256")) && CO % 256 == 0 ? 1 : 0;
   rdeic_set_conv_option(9, h8);
-  rdeic_set_conv_option(10, h256);
-  const int trow = h256 ? 4 : (h8 && H % 8 == 0) ? 8 : 4;
-  const long tiles = (long)N * (H / trow) * (W / 64) * (CO / (h256 ? 256 : 128));
+  const int trow = (h8 && H % 8 == 0) ? 8 : 4;
+  const long tiles = (long)N * (H / trow) * (W / 64) * (CO / 128);
   unsigned long long* st;
   CK(hipMalloc(&st, tiles * 8 * 8));
   CK(hipMemset(st, 0, tiles * 8 * 8));
@@ -131,7 +130,7 @@ int main(int argc, char** argv) {
   const double cyc_span = (double)(t1 - t0);
   const double clk_ghz = cyc_span / (ms * 1e6);
   // MFMA-bound floor per block: (9 taps x cin/32) x 16 MFMA x 16 cycles x waves per SIMD (2 or 4)
-  const double floor_main = 9.0 * (C / 32) * 16 * 16 * (h256 ? 4 : trow / 2);
+  const double floor_main = 9.0 * (C / 32) * 16 * 16 * (trow / 2);
   printf("{\"shape\": [%d, %d, %d, %d, %d], \"res\": %d, \"stats\": %d, \"ms\": %.4f, \"tflops\": %.1f, "
          "\"blocks\": %ld, \"cus_seen\": %zu, \"clock_ghz_est\": %.3f, \"blocks_in_flight_per_cu\": %.2f, "
          "\"cycles\": {\"prologue_med\": %.0f, \"main_med\": %.0f, \"main_p90\": %.0f, \"epilogue_med\": %.0f, "
