@@ -154,6 +154,15 @@ int rdeic_groupnorm_stats(const void* x0, int32_t c0, int32_t ld0, const void* x
                           float* ab, float* ws, int32_t dtype, void* stream);
 /* y = silu?(x*a + b) * out_mul materialised (NHWC), where the consumer is not a conv
  * (e.g. the VAE encoder's c = swish(norm_out(h)), followed by the 0.18215 latent scale). */
+/* GroupNorm finalize + apply in one launch for small images (hw = 64, 128 or 256 pixels: the UNet's 16^2 / 8^2
+ * levels; openaimodel.py:200-204, 254-274; attention.py:250-266): y[n][hw][c0 + c1] = silu?(x * a + b) of the
+ * channel concat of x0 (c0 ch, partials p0) and x1 (c1 ch, partials p1), the (a, b) table recomputed per block from
+ * the partials (rdeic_groupnorm_parts_ab's arithmetic: bit-identical to parts_ab + apply) and also written to ab
+ * [n][c][2]. bf16, c0 / c1 / ld / yld multiples of 8, c <= 2560, groups <= 256. */
+int rdeic_groupnorm_parts_apply(const float* p0, int32_t c0, const float* p1, int32_t c1, const void* x0, int32_t ld0,
+                                const void* x1, int32_t ld1, int32_t n, int32_t hw, int32_t groups, float eps,
+                                const float* gamma, const float* beta, int32_t silu, float* ab, void* y, int32_t yld,
+                                void* stream);
 int rdeic_groupnorm_apply(const void* x, int32_t n, int32_t hw, int32_t c, int32_t ld, const float* ab,
                           int32_t ab_c, int32_t silu, float out_mul, void* y, int32_t yld, int32_t dtype,
                           void* stream);
@@ -341,7 +350,8 @@ int rdeic_prof_start(int32_t capacity, int32_t every);
 #define RDEIC_COUNT_LN_FUSED 4     /* rdeic_layernorm_rowstats (LayerNorm folded into the next linear) */
 #define RDEIC_COUNT_SPLITK 5       /* rdeic_conv2d_splitk launches that ran split (partial pass + reduce) */
 #define RDEIC_COUNT_EDGE 6         /* the VAE edge convs (conv_edge.hip: conv_in from 8 channels, norm -> SiLU -> conv to <= 16) */
-#define RDEIC_COUNT_KINDS 8        /* 7: unused */
+#define RDEIC_COUNT_GN_PARTS_APPLY 7 /* rdeic_groupnorm_parts_apply (finalize + apply in one launch) */
+#define RDEIC_COUNT_KINDS 8
 int64_t rdeic_launch_count(int32_t kind);
 /* Per-row LayerNorm statistics (attention.py:273-285, torch.nn.LayerNorm: biased variance, eps) of
  * bf16 rows x[rows][c] (pixel stride ld): ms[2 r] = mean, ms[2 r + 1] = 1 / sqrt(var + eps), two-pass

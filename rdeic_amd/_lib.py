@@ -121,6 +121,8 @@ PROTOTYPES = {
     "rdeic_image_ssim": (C.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, C.c_size_t, _p, _p]),
     "rdeic_groupnorm_parts_floats": (C.c_size_t, [_i64, _i32, _i32]),
     "rdeic_groupnorm_parts_ab": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p]),
+    "rdeic_groupnorm_parts_apply": (C.c_int, [_p, _i32, _p, _i32, _p, _i32, _p, _i32, _i32, _i32, _i32, _f, _p, _p,
+                                              _i32, _p, _p, _i32, _p]),
     "rdeic_rans_enc_tables_create": (_p, [_p, _i32, _p, _p, _i32]),
     "rdeic_rans_enc_tables_destroy": (None, [_p]),
     "rdeic_rans_encode_batch_t": (C.c_int, [_p, _i32, _p, _p, _sz, _sz, _p, _sz, _p, _i32]),

@@ -14,121 +14,172 @@ namespace rdeic_conv {
 namespace {
 
 // ============================================================================================
-// conv_in: cin = 8 (3 real channels, zero-padded: rdeic_image_u8_to_nhwc), 3x3, stride 1, pad 1.
+// conv_in: cin = 8 (3 real channels, zero-padded: rdeic_image_u8_to_nhwc), 3x3, stride 1, pad 1, bias, bf16 out.
 // GEMM view M = pixels, N = cout, K = 9 taps x 8 channels = 72, laid out as the LDS-DMA / register tiles'
 // two 64-deep k-tiles (four 32-deep MFMA k-steps, the last all zero). An A-fragment lane of
 // v_mfma_f32_16x16x32_bf16 holds 8 consecutive k = ONE tap's 8 channels of one pixel: a single 16-byte load
 // from the NHWC input (zeros outside the image). B fragments (the packed weight, 32 KB) come straight from L2.
-// No LDS staging, no im2col, no address VALU beyond one bounds check per tap. Tile: 128 pixels x 128 channels,
-// 8 waves of 64 x 32 (one canonical 64-row GroupNorm block per wave row).
-// The MFMA sequence over k is conv_kernel's (k-steps 0..3 in order, zero products included) and the epilogue
-// IS epilogue_vec (bias, bf16 rounding, canonical statistics, 16-byte stores), so outputs and statistics are
-// bit-identical to the register tile this replaces (test_edge_convs_gpu.py).
+// No LDS staging of operands, no im2col. The MFMA sequence over k is conv_kernel's (k-steps 0..3 in order, zero
+// products included), so the accumulators equal the register tile's bit for bit.
+// The kernel is bound by its 1 GB of output stores, so its epilogue is WAVE-PRIVATE: each wave (64 pixels = one
+// canonical 64-row GroupNorm block x 64 channels) rounds its tile to bf16 into its own LDS region, then
+//   * stores it as 16-byte row chunks (8 lanes per 128-byte pixel row),
+//   * and scans it for the GroupNorm partials: lane (4-channel quad, 16-row group g) sums its group's rows in
+//     order (fmaf for the squares), and ((g0 + g1) + g2) + g3 is taken across the four lane quarters: the
+//     canonical order of epilogue_vec / gn_rows_partial, so the statistics are bit-identical too;
+// with no block barrier anywhere (epilogue_vec's four parked passes took 8 block barriers per 128 pixels).
 // ============================================================================================
-constexpr int CI_BM = 128, CI_BN = 128, CI_WGM = 2, CI_WGN = 4, CI_NT = CI_WGM * CI_WGN * 64, CI_P = 4;
-constexpr int CI_LDS = (CI_BM / CI_P) * (CI_BN + 4) * 4;  // epilogue_vec's parked pass (17 KB)
+constexpr int CI_NT = 256;            // 4 waves: 2 pixel blocks of 64 x 2 channel halves of 64
+constexpr int CI_ROWB = 136;          // LDS bytes per parked pixel row (64 bf16 + 8): conflict-free scans
+constexpr int CI_WLDS = 64 * CI_ROWB; // per wave
 
-__global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a) {
+__global__ __launch_bounds__(CI_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv_in8_kernel(ConvArgs a, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  constexpr int TM = CI_BM / CI_WGM / 16, TN = CI_BN / CI_WGN / 16;  // 4 x 2 fragments per wave
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / CI_WGN, wn = wave - (wave / CI_WGN) * CI_WGN;
-  const int tn = (a.cout + CI_BN - 1) / CI_BN;
-  const int mt = blockIdx.x / tn, nt = blockIdx.x - mt * tn;
-  const int m0 = mt * CI_BM, n0 = nt * CI_BN;
+  const int mt = blockIdx.x / tiles_n, nt = blockIdx.x - mt * tiles_n;
+  const int m0 = mt * 128 + (wave >> 1) * 64;  // this wave's 64 pixels
+  const int c0 = nt * 128 + (wave & 1) * 64;   // ... and 64 channels
+  if (c0 >= a.cout || m0 >= a.M) return;     // wave-uniform (cout % 64 == 0)
+  char* const W = lds + wave * CI_WLDS;
   const int lr = lane & 15, lq = lane >> 4;
   const int hw = a.h * a.w;
+  const bf16* wt = reinterpret_cast<const bf16*>(a.weight);
+  const bf16* in = reinterpret_cast<const bf16*>(a.in0);
 
-  // B fragments of this wave's 32 columns, all four k-steps (k = 32 s + 8 lq)
-  bf16x8 bfr[4][TN];
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * (CI_BN / CI_WGN) + j * 16 + lr;
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 v = {};
-      if (n < a.cout) v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.weight) + (long)n * a.wld + 32 * s + 8 * lq);
-      bfr[s][j] = v;
-    }
-  }
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
+    bf16x8 bfv[4], af[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // k = 32 s + 8 lq of weight row c0 + 16 j + lr
+      bfv[j] = *reinterpret_cast<const bf16x8*>(wt + (long)(c0 + 16 * j + lr) * a.wld + 32 * s + 8 * lq);
     const int tap = 4 * s + lq;  // this lane's k-chunk in k-step s; taps >= 9 are the zero tail
     const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-    bf16x8 af[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * (CI_BM / CI_WGM) + i * 16 + lr;
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + i * 16 + lr;
       bf16x8 v = {};
       if (tap < 9 && m < a.M) {
         const int img = m / hw, rem = m - img * hw;
         const int iy = rem / a.w + ky - 1, ix = rem - (rem / a.w) * a.w + kx - 1;
         if ((unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w)
-          v = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.in0) + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
+          v = *reinterpret_cast<const bf16x8*>(in + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
       }
       af[i] = v;
     }
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s][j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
   }
-  epilogue_vec<CI_BM, CI_BN, CI_WGM, CI_WGN, CI_NT, CI_P>(acc, a, m0, n0, wm, wn, lane, tid, lds);
+  // (acc + bias) rounded to bf16, parked row-major: lane holds channel 16 j + lr of pixels 16 i + 4 lq + r
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float b = a.bias ? a.bias[c0 + 16 * j + lr] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<bf16*>(W + (16 * i + 4 * lq + r) * CI_ROWB + (16 * j + lr) * 2) = (bf16)(acc[i][j][r] + b);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS tile, written by all its lanes
+  __builtin_amdgcn_wave_barrier();
+  bf16* const out = reinterpret_cast<bf16*>(a.out);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {  // 8 lanes per pixel row: 16 bytes each
+    const int row = 8 * k + (lane >> 3), ch = lane & 7;
+    const uint2 lo = *reinterpret_cast<const uint2*>(W + row * CI_ROWB + ch * 16);
+    const uint2 hi = *reinterpret_cast<const uint2*>(W + row * CI_ROWB + ch * 16 + 8);
+    if (m0 + row < a.M) *reinterpret_cast<uint4*>(out + (long)(m0 + row) * a.out_ld + c0 + ch * 8) = uint4{lo.x, lo.y, hi.x, hi.y};
+  }
+  if (!a.gn_part) return;
+  const int q4 = lane & 15, g = lane >> 4;  // channels c0 + 4 q4 .. + 3, rows 16 g .. 16 g + 15
+  const int nv = a.M - (m0 + 16 * g);       // valid rows of the group
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const uint2 w2 = *reinterpret_cast<const uint2*>(W + (16 * g + r) * CI_ROWB + q4 * 8);
+    if (r < nv) {
+      const float y[4] = {__uint_as_float(w2.x << 16), __uint_as_float(w2.x & 0xffff0000u), __uint_as_float(w2.y << 16),
+                          __uint_as_float(w2.y & 0xffff0000u)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[e] += y[e];
+        s2[e] = fmaf(y[e], y[e], s2[e]);
+      }
+    }
+  }
+  float t1[4], t2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // ((g0 + g1) + g2) + g3 in the quarter-0 lanes
+    t1[e] = ((s1[e] + __shfl(s1[e], q4 + 16, 64)) + __shfl(s1[e], q4 + 32, 64)) + __shfl(s1[e], q4 + 48, 64);
+    t2[e] = ((s2[e] + __shfl(s2[e], q4 + 16, 64)) + __shfl(s2[e], q4 + 32, 64)) + __shfl(s2[e], q4 + 48, 64);
+  }
+  if (g == 0) {
+    float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0) / 64) * a.cout + c0 + 4 * q4) * 2;
+    *reinterpret_cast<float4*>(pp) = make_float4(t1[0], t2[0], t1[1], t2[1]);
+    *reinterpret_cast<float4*>(pp + 4) = make_float4(t1[2], t2[2], t1[3], t2[3]);
+    if (lane == 0 && m0 == 0 && c0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
+  }
 }
 
 // ============================================================================================
 // norm -> SiLU -> 3x3 conv to a few channels (cout <= 16; the decoder's conv_out 128 -> 3, fp32 output).
-// A block owns TR x 64 output pixels (16 waves, one output row each). Per 32-channel block of the input, all
-// 1024 threads load the (TR + 2) x 66 halo of the RAW input (16 bytes each, coalesced 64-byte pixel slices),
-// apply the GroupNorm affine + SiLU ONCE per element in registers (rdeic_groupnorm_apply's formula:
-// fma, then x * rcp(1 + e^-x), rounded to bf16) and write it to LDS; then every wave runs the 9 taps as
-// 16x16x32 MFMAs with N = 16 (cout real columns, the rest zero weights) reading its A fragments from the halo.
-// The transform is 1.16x the element count (halo rows / columns), the MFMA work ~10% of the VALU's, and two
-// blocks (76 KB of LDS each) share a CU, so one block's transform runs beside the other's MFMAs and loads.
+// A block owns TR x 64 output pixels (TR waves, one output row each). Per 32-channel block of the input, the
+// threads load the (TR + 2) x 66 halo of the RAW input (16 bytes each: coalesced 64-byte pixel slices), apply the
+// GroupNorm affine + SiLU ONCE per element in registers (rdeic_groupnorm_apply's formula: fma, then
+// x * rcp(1 + e^-x), rounded to bf16; the affine / add / multiply two elements per packed-f32 instruction, which
+// is bit-identical to the scalar form) and write it to LDS; then every wave runs the 9 taps as 16x16x32 MFMAs with
+// N = 16 (cout real columns, the rest zero weights) reading its A fragments from the halo. The next block's raw
+// loads are issued before this block's MFMAs (register double buffering), and two blocks share a CU, so the HBM
+// stream runs under the transform. The transform is (TR + 2) / TR x 66 / 64 of the element count; it is the VALU
+// floor (two transcendentals per element), the MFMA work ~15% of it.
 // k order: 32-channel block major, tap minor (as the halo convs); fp32 accumulation.
 // ============================================================================================
-constexpr int NR_TR = 16, NR_TC = 64, NR_HR = NR_TR + 2, NR_HC = NR_TC + 2, NR_HPIX = NR_HR * NR_HC;  // 1188
-constexpr int NR_NT = 1024, NR_ITEMS = NR_HPIX * 4;  // 16-byte chunks per 32-channel halo (4752)
-constexpr int NR_IPT = (NR_ITEMS + NR_NT - 1) / NR_NT;  // 5 per thread
-constexpr int NR_LDS = NR_HPIX * 64;                      // 76,032 B of halo, then the (a, b) table
-constexpr int NR_AB_MAX = 512;                            // input channels whose table fits
+constexpr int NR_TC = 64, NR_HC = NR_TC + 2;
+constexpr int NR_AB_MAX = 512;  // input channels whose (a, b) table fits the LDS
+template <int TR> struct Narrow {
+  static constexpr int NT = TR * 64, HPIX = (TR + 2) * NR_HC, ITEMS = HPIX * 4;  // 16-byte chunks per halo
+  static constexpr int IPT = (ITEMS + NT - 1) / NT;
+  static constexpr int LDS = HPIX * 64;  // halo (then the (a, b) table)
+};
 __device__ __forceinline__ int nr_sw(int s) { return ((s >> 2) & 1) << 1; }  // halo conv swizzle (conflict-free)
 
-template <bool SILU>
-__global__ __launch_bounds__(NR_NT) void conv3x3_gn_narrow_kernel(ConvArgs a, int tiles_x, int tiles_y) {
+template <int TR, bool SILU>
+__global__ __launch_bounds__(TR * 64) void conv3x3_gn_narrow_kernel(ConvArgs a, int tiles_x, int tiles_y) {
+  using NR = Narrow<TR>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* const abl = reinterpret_cast<float*>(lds + NR_LDS);  // the image's GroupNorm (a, b) table
+  float* const abl = reinterpret_cast<float*>(lds + NR::LDS);  // the image's GroupNorm (a, b) table
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int sp = blockIdx.x;
   const int tx = sp % tiles_x;
   sp /= tiles_x;
   const int ty = sp % tiles_y, img = sp / tiles_y;
-  const int oy0 = ty * NR_TR, ox0 = tx * NR_TC;
+  const int oy0 = ty * TR, ox0 = tx * NR_TC;
   const int H = a.h, W = a.w, cin = a.c0;
   const int lr = lane & 15, lq = lane >> 4;
-  const int q = tid & 3;  // this thread's 16-byte chunk of every halo pixel it loads (NR_NT % 4 == 0)
+  const int q = tid & 3;  // this thread's 16-byte chunk of every halo pixel it loads (NT % 4 == 0)
   const bf16* in = reinterpret_cast<const bf16*>(a.in0);
   // LDS-only barrier: __syncthreads() would also wait for the next channel block's loads in flight
   auto bar = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
-  for (int i = tid; i < cin / 2; i += NR_NT)
+  for (int i = tid; i < cin / 2; i += NR::NT)
     reinterpret_cast<float4*>(abl)[i] = reinterpret_cast<const float4*>(a.gn_ab + (long)img * cin * 2)[i];
-  uint4 raw[NR_IPT];
+  uint4 raw[NR::IPT];
   auto load = [&](int cb) {  // the raw halo chunks of this thread (zeros outside the image)
 #pragma unroll
-    for (int k = 0; k < NR_IPT; ++k) {
-      const int it = tid + k * NR_NT, hp = it >> 2;
+    for (int k = 0; k < NR::IPT; ++k) {
+      const int it = tid + k * NR::NT, hp = it >> 2;
       const int hr = hp / NR_HC, hc = hp - (hp / NR_HC) * NR_HC;
       const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
       raw[k] = uint4{0u, 0u, 0u, 0u};
-      if (it < NR_ITEMS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      if (it < NR::ITEMS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
         raw[k] = *reinterpret_cast<const uint4*>(in + ((long)(img * H + iy) * W + ix) * a.ld0 + cb + 8 * q);
     }
   };
@@ -141,26 +192,31 @@ __global__ __launch_bounds__(NR_NT) void conv3x3_gn_narrow_kernel(ConvArgs a, in
     bar();  // cb = 0: the (a, b) table is in LDS; else the previous block's MFMA reads of the halo are done
     const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb + 8 * q) * 2);
     const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
-    const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
-    const float bv[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
+    const f32x2 av[4] = {{t0.x, t0.z}, {t1.x, t1.z}, {t2.x, t2.z}, {t3.x, t3.z}};
+    const f32x2 bv[4] = {{t0.y, t0.w}, {t1.y, t1.w}, {t2.y, t2.w}, {t3.y, t3.w}};
 #pragma unroll
-    for (int k = 0; k < NR_IPT; ++k) {
-      const int it = tid + k * NR_NT, hp = it >> 2;
-      if (it >= NR_ITEMS) continue;
+    for (int k = 0; k < NR::IPT; ++k) {
+      const int it = tid + k * NR::NT, hp = it >> 2;
+      if (it >= NR::ITEMS) continue;
       const int hr = hp / NR_HC, hc = hp - (hp / NR_HC) * NR_HC;
       const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
-      bf16x8 o = {};
+      uint4 o = uint4{0u, 0u, 0u, 0u};
       if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {  // outside: the normalised tensor's zero pad
-        bf16x8 v;
-        *reinterpret_cast<uint4*>(&v) = raw[k];
+        const unsigned w4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+        unsigned o4[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float x = __builtin_fmaf((float)v[e], av[e], bv[e]);
-          if constexpr (SILU) x *= __builtin_amdgcn_rcpf(1.0f + __expf(-x));
-          o[e] = (bf16)x;
+        for (int e = 0; e < 4; ++e) {  // channels 2e, 2e + 1 of the chunk
+          f32x2 x = pk_fma(f32x2{__uint_as_float(w4[e] << 16), __uint_as_float(w4[e] & 0xffff0000u)}, av[e], bv[e]);
+          if constexpr (SILU) {
+            const f32x2 d = f32x2{__expf(-x.x), __expf(-x.y)} + 1.0f;
+            x *= f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+          }
+          const bf16 lo = (bf16)x.x, hi = (bf16)x.y;
+          o4[e] = (unsigned)__builtin_bit_cast(unsigned short, lo) | ((unsigned)__builtin_bit_cast(unsigned short, hi) << 16);
         }
+        o = uint4{o4[0], o4[1], o4[2], o4[3]};
       }
-      *reinterpret_cast<bf16x8*>(lds + hp * 64 + ((q ^ nr_sw(hp)) << 4)) = o;
+      *reinterpret_cast<uint4*>(lds + hp * 64 + ((q ^ nr_sw(hp)) << 4)) = o;
     }
     bar();
     if (cb + 32 < cin) load(cb + 32);  // the next block's loads fly under this block's MFMAs
@@ -205,26 +261,29 @@ int launch_edge(const rdeic_conv_desc* d, const ConvArgs& a, hipStream_t s, bool
       d->up2 || d->c1 || d->ho != d->h || d->wo != d->w || a.batch != 1 || d->out_mode != 0 || d->ld0 % 8 ||
       ((uintptr_t)d->in0) % 16 || ((uintptr_t)d->weight) % 16)
     return -1;
-  // conv_in: 8 input channels, the vector epilogue (bf16 or fp32 output), statistics per image
-  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout >= 64 && epi_vec_ok(a) && a.epi_vec) {
+  // conv_in: 8 input channels, bias only, bf16 output, statistics per image (64-row blocks)
+  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout % 64 == 0 && !d->emb && !d->act && !d->res &&
+      !d->out_f32 && !d->ln_rows && d->out_ld % 8 == 0 && ((uintptr_t)d->out) % 16 == 0) {
     ConvArgs e = a;
     const bool stats = e.gn_part != nullptr && e.gn_hw > 0 && e.gn_hw % 64 == 0;
     if (!stats) e.gn_part = nullptr;
     if (fused) *fused = stats;
     rdeic_count_launch(RDEIC_COUNT_EDGE);
-    const long blocks = (long)cdiv(e.M, CI_BM) * cdiv(e.cout, CI_BN);
-    hipLaunchKernelGGL(conv_in8_kernel, dim3((unsigned)blocks), dim3(CI_NT), CI_LDS, s, e);
+    const int tn = (e.cout + 127) / 128;
+    const long blocks = (long)((e.M + 127) / 128) * tn;
+    hipLaunchKernelGGL(conv_in8_kernel, dim3((unsigned)blocks), dim3(CI_NT), 4 * CI_WLDS, s, e, tn);
     return launch_status();
   }
   // norm -> (SiLU) -> conv to <= 16 channels
-  if (d->gn_ab && d->cout <= 16 && d->c0 % 32 == 0 && d->c0 <= NR_AB_MAX && d->h % NR_TR == 0 && d->w % NR_TC == 0 &&
+  constexpr int TR = 8;
+  if (d->gn_ab && d->cout <= 16 && d->c0 % 32 == 0 && d->c0 <= NR_AB_MAX && d->h % TR == 0 && d->w % NR_TC == 0 &&
       !d->gn_part && !d->emb && ((uintptr_t)d->gn_ab) % 16 == 0) {
     rdeic_count_launch(RDEIC_COUNT_EDGE);
-    const int cin_tab = d->c0 * 8;
-    const int tx = d->w / NR_TC, ty = d->h / NR_TR;
+    const int tx = d->w / NR_TC, ty = d->h / TR;
     const dim3 g((unsigned)((long)d->n * ty * tx));
-    if (d->gn_silu) hipLaunchKernelGGL(conv3x3_gn_narrow_kernel<true>, g, dim3(NR_NT), NR_LDS + cin_tab, s, a, tx, ty);
-    else hipLaunchKernelGGL(conv3x3_gn_narrow_kernel<false>, g, dim3(NR_NT), NR_LDS + cin_tab, s, a, tx, ty);
+    const int lds = Narrow<TR>::LDS + d->c0 * 8;
+    if (d->gn_silu) hipLaunchKernelGGL((conv3x3_gn_narrow_kernel<TR, true>), g, dim3(TR * 64), lds, s, a, tx, ty);
+    else hipLaunchKernelGGL((conv3x3_gn_narrow_kernel<TR, false>), g, dim3(TR * 64), lds, s, a, tx, ty);
     return launch_status();
   }
   return -1;

@@ -515,6 +515,114 @@ __global__ __launch_bounds__(256) void gn_finalize_parts_kernel(const float* __r
   }
 }
 
+// GroupNorm finalize + apply in ONE launch for small images (hw <= 256 pixels: the UNet / control net's 16^2 and
+// 8^2 levels, T = hw / 64 <= 4 partial row blocks per image), openaimodel.py:200-204 / 254-274 (in_layers /
+// out_layers GroupNorm32 -> SiLU) and attention.py:250-266 (SpatialTransformer.norm). There the two-launch form
+// (gn_finalize_parts, then gn_apply) is two ~10 us latency floors for a few hundred KB of data.
+// Every block recomputes its image's (a, b) table from the T x c partials (<= 80 KB, L2-resident) instead of
+// waiting for a finalize launch: lane tt of a T-lane segment sums row block tt's channel pairs of one group in
+// fp64 in gn_finalize_parts_kernel's order, and a butterfly over the T lanes (xor offsets T/2 .. 1) gives the
+// same number as that kernel's 256-thread reduction (its lanes >= T add exact zeros), so mean / rstd and the
+// (a, b) table are bit-identical to the two-launch path; so is the apply arithmetic (gn_apply_vec_kernel's).
+// Channels [0, c0) come from x0 / p0 and [c0, c0 + c1) from x1 / p1 (the UNet's skip concat); the output y holds
+// all c0 + c1 channels. Block (0, img) also writes the table to ab (for any other consumer of it).
+constexpr int GNPA_U = 8;  // 16-byte chunks per thread
+__global__ __launch_bounds__(256) void gn_parts_apply_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                             const bf16* __restrict__ x0, int c0, int ld0,
+                                                             const bf16* __restrict__ x1, int c1, int ld1, int hw,
+                                                             int groups, float eps, const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, int silu,
+                                                             float* __restrict__ ab, bf16* __restrict__ y, int yld) {
+  __shared__ __attribute__((aligned(16))) float lab[2 * GN_APPLY_LDS_C];
+  __shared__ float gms[2 * 256];  // per group (mean as float, rstd)
+  const int img = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = c0 + c1, cpg = c / groups;
+  const int T = hw / 64;                 // partial row blocks per image: 1, 2 or 4
+  const int gpw = 64 / T;                // groups per wave pass
+  // x chunks first (their loads fly under the finalize)
+  const int cp = c >> 3, total = hw * cp;
+  const int base = blockIdx.x * (256 * GNPA_U) + t;
+  bf16x8 v[GNPA_U];
+  int pix[GNPA_U], ch[GNPA_U];
+#pragma unroll
+  for (int u = 0; u < GNPA_U; ++u) {
+    const int i = base + u * 256;
+    pix[u] = i / cp;
+    ch[u] = (i - pix[u] * cp) * 8;
+    if (i < total) {
+      const bool s1 = ch[u] >= c0;
+      v[u] = *reinterpret_cast<const bf16x8*>(s1 ? x1 + ((long)img * hw + pix[u]) * ld1 + (ch[u] - c0)
+                                                  : x0 + ((long)img * hw + pix[u]) * ld0 + ch[u]);
+    }
+  }
+  // finalize: wave w takes groups w * gpw + k * 4 * gpw + lane / T
+  for (int gb = wave * gpw; gb < groups; gb += 4 * gpw) {
+    const int g = gb + lane / T, tt = lane % T;
+    double S = 0.0, Q = 0.0;
+    if (g < groups) {
+      const int ga = g * cpg, ge = ga + cpg;
+      for (int sgi = 0; sgi < 2; ++sgi) {
+        const float* p = sgi ? p1 : p0;
+        const int sb = sgi ? c0 : 0, cs = sgi ? c1 : c0;
+        const int lo = max(ga, sb), hi = min(ge, sb + cs);
+        if (hi <= lo) continue;
+        const float* e = p + 4 + (((long)img * T + tt) * cs + (lo - sb)) * 2;
+        for (int j = 0; j < hi - lo; ++j) {
+          S += (double)e[2 * j];
+          Q += (double)e[2 * j + 1];
+        }
+      }
+    }
+    for (int o = T >> 1; o > 0; o >>= 1) {  // the 256-thread reduction restricted to its nonzero lanes
+      S += __shfl_xor(S, o, 64);
+      Q += __shfl_xor(Q, o, 64);
+    }
+    S = (S + 0.0) + (0.0 + 0.0);  // block_sum256_d's cross-wave combine, the other waves' sums being +0
+    Q = (Q + 0.0) + (0.0 + 0.0);
+    if (g < groups && tt == 0) {
+      const double N = (double)hw * cpg;
+      const double mean = S / N;
+      const float var = (float)fmax(Q / N - mean * mean, 0.0);
+      gms[2 * g] = (float)mean;
+      gms[2 * g + 1] = rsqrtf(var + eps);
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < c; j += 256) {
+    const int g = j / cpg;
+    const float mf = gms[2 * g], rstd = gms[2 * g + 1];
+    const float gm = gamma ? gamma[j] : 1.f, be = beta ? beta[j] : 0.f;
+    const float av = gm * rstd, bv = be - mf * av;
+    lab[2 * j] = av;
+    lab[2 * j + 1] = bv;
+    if (blockIdx.x == 0) {
+      ab[((long)img * c + j) * 2 + 0] = av;
+      ab[((long)img * c + j) * 2 + 1] = bv;
+    }
+  }
+  __syncthreads();
+  bf16* yi = y + (long)img * hw * yld;
+#pragma unroll
+  for (int u = 0; u < GNPA_U; ++u) {
+    if (base + u * 256 >= total) break;
+    const float4* p = reinterpret_cast<const float4*>(lab + ch[u] * 2);
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 s = p[q];  // (a, b) of channels ch+2q, ch+2q+1
+      float v0 = (float)v[u][2 * q] * s.x + s.y;
+      float v1 = (float)v[u][2 * q + 1] * s.z + s.w;
+      if (silu) {  // x * rcp(1 + e^-x), as gn_apply_vec_kernel
+        v0 *= __builtin_amdgcn_rcpf(1.0f + __expf(-v0));
+        v1 *= __builtin_amdgcn_rcpf(1.0f + __expf(-v1));
+      }
+      o[2 * q] = (bf16)v0;
+      o[2 * q + 1] = (bf16)v1;
+    }
+    *reinterpret_cast<bf16x8*>(yi + (long)pix[u] * yld + ch[u]) = o;
+  }
+}
+
 }  // namespace
 
 // stand-alone partials of a [rows][c] (pixel stride ld) tensor (declared in common.h for the conv
@@ -543,6 +651,26 @@ extern "C" int rdeic_groupnorm_parts_ab(const float* p0, int32_t c0, const float
     return RDEIC_EINVAL;
   hipLaunchKernelGGL(gn_finalize_parts_kernel, dim3(groups, n), dim3(256), 0, (hipStream_t)stream, p0, c0,
                      p1 ? p1 : p0, c1, hw, groups, eps, gamma, beta, ab);
+  return launch_status();
+}
+
+extern "C" int rdeic_groupnorm_parts_apply(const float* p0, int32_t c0, const float* p1, int32_t c1, const void* x0,
+                                           int32_t ld0, const void* x1, int32_t ld1, int32_t n, int32_t hw,
+                                           int32_t groups, float eps, const float* gamma, const float* beta,
+                                           int32_t silu, float* ab, void* y, int32_t yld, void* stream) {
+  const int c = c0 + c1;
+  if (!p0 || !x0 || !ab || !y || n <= 0 || (hw != 64 && hw != 128 && hw != 256) || c0 <= 0 || c1 < 0 ||
+      (c1 > 0 && (!p1 || !x1)) || groups <= 0 || groups > 256 || c % groups || c0 % 8 || c1 % 8 ||
+      c > GN_APPLY_LDS_C || ld0 % 8 || (c1 && ld1 % 8) || yld % 8 || ((uintptr_t)x0) % 16 ||
+      (c1 && ((uintptr_t)x1) % 16) || ((uintptr_t)y) % 16)
+    return RDEIC_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps(s, RDEIC_PROF_GN_APPLY, 2.0 * n * hw * c * 2);
+  rdeic_count_launch(RDEIC_COUNT_GN_PARTS_APPLY);
+  const int blocks = (hw * (c / 8) + 256 * GNPA_U - 1) / (256 * GNPA_U);
+  hipLaunchKernelGGL(gn_parts_apply_kernel, dim3(blocks, n), dim3(256), 0, s, p0, p1 ? p1 : p0, (const bf16*)x0, c0, ld0,
+                     (const bf16*)(x1 ? x1 : x0), c1, c1 ? ld1 : ld0, hw, groups, eps, gamma, beta, silu, ab, (bf16*)y,
+                     yld);
   return launch_status();
 }
 

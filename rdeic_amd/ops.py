@@ -109,9 +109,19 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
         # normalised (concatenated) input once with the vectorised, HBM-rate apply kernel instead
         xin = torch.empty(x.shape[:3] + (p.cin,), dtype=x.dtype, device=x.device)
         c0 = x.shape[3]
-        group_norm_apply(x, gn, gn_silu, out=xin[..., :c0])
-        if x2 is not None:
-            group_norm_apply(x2, gn[:, c0:], gn_silu, out=xin[..., c0:])
+        pend = getattr(gn, "_rdeic_pending", None)
+        if pend is not None and c0 % 8 == 0 and pix_ld(x) % 8 == 0 and x.data_ptr() % 16 == 0 and \
+                (x2 is None or (x2.shape[3] % 8 == 0 and pix_ld(x2) % 8 == 0 and x2.data_ptr() % 16 == 0)):
+            p0, pc0, p1, c1, n_, hw_, groups, eps, gamma, beta = pend
+            _launch(("gn_apply", float(2 * xin.numel() * xin.element_size()), None), "rdeic_groupnorm_parts_apply",
+                    p0.data_ptr(), pc0, _ptr(p1), c1, x.data_ptr(), pix_ld(x), _ptr(x2),
+                    pix_ld(x2) if x2 is not None else 0, n_, hw_, groups, float(eps), gamma.data_ptr(),
+                    beta.data_ptr(), int(gn_silu), gn.data_ptr(), xin.data_ptr(), pix_ld(xin), stream_ptr())
+            del gn._rdeic_pending
+        else:
+            group_norm_apply(x, gn, gn_silu, out=xin[..., :c0])
+            if x2 is not None:
+                group_norm_apply(x2, gn[:, c0:], gn_silu, out=xin[..., c0:])
         x, x2, gn = xin, None, None
     n, h, w, c0 = x.shape
     ld0 = pix_ld(x)
@@ -158,6 +168,7 @@ def conv2d(x: torch.Tensor, p: ConvParams, *, x2: Optional[torch.Tensor] = None,
     if gn is not None:
         if gn.shape != (n, p.cin, 2):
             raise ValueError("gn affine must be [n, cin, 2]")
+        _ab_ready(gn)
         d.gn_ab = gn.data_ptr()
         d.gn_silu = int(gn_silu)
     if emb is not None:
@@ -527,8 +538,8 @@ HALO_MAX_C = 512
 
 
 # launch counters of the library (rdeic_launch_count, RDEIC_COUNT_* in include/rdeic_hip.h)
-COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED, COUNT_SPLITK, COUNT_EDGE = \
-    0, 1, 2, 3, 4, 5, 6
+COUNT_HALO_CONV, COUNT_GN_APPLY, COUNT_LAYERNORM, COUNT_HALO_SMALL, COUNT_LN_FUSED, COUNT_SPLITK, COUNT_EDGE, \
+    COUNT_GN_PARTS_APPLY = 0, 1, 2, 3, 4, 5, 6, 7
 
 
 def launch_count(kind: int) -> int:
@@ -666,9 +677,30 @@ def gemm_batched(a: torch.Tensor, b_nk: torch.Tensor, out: torch.Tensor, *, batc
     return out
 
 
+# GroupNorm finalize + apply in ONE launch on small images (rdeic_groupnorm_parts_apply: the UNet / control net's
+# 16^2 and 8^2 levels, where the finalize and the apply are each a ~10 us latency floor). group_norm_ab(...,
+# defer=True) then returns the affine with its finalize pending; conv2d's materialised GroupNorm runs the fused
+# launch (which also fills the affine), and any other consumer of the affine finalizes it first (_ab_ready).
+GN_PARTS_APPLY = True
+GN_PARTS_APPLY_HW = (64, 128, 256)
+
+
+def _ab_ready(ab: Optional[torch.Tensor]) -> None:
+    """Run a deferred GroupNorm finalize (group_norm_ab(defer=True)) before the affine is read."""
+    pend = getattr(ab, "_rdeic_pending", None) if ab is not None else None
+    if pend is None:
+        return
+    p0, c0, p1, c1, n, hw, groups, eps, gamma, beta = pend
+    call("rdeic_groupnorm_parts_ab", p0.data_ptr(), c0, _ptr(p1), c1, n, hw, groups, float(eps),
+         gamma.data_ptr(), beta.data_ptr(), ab.data_ptr(), stream_ptr())
+    del ab._rdeic_pending
+
+
 def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float,
-                  x2: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Per-(image, channel) affine [n, c, 2] such that GroupNorm(cat(x, x2)) = x*a + b."""
+                  x2: Optional[torch.Tensor] = None, defer: bool = False) -> torch.Tensor:
+    """Per-(image, channel) affine [n, c, 2] such that GroupNorm(cat(x, x2)) = x*a + b.
+    defer: the caller hands the affine straight to conv2d(gn=...): on small images with fused statistics its
+    finalize is left pending and runs inside that conv's materialised GroupNorm (rdeic_groupnorm_parts_apply)."""
     n, h, w, c0 = x.shape
     ld0 = pix_ld(x)
     c1, ld1 = (x2.shape[3], pix_ld(x2)) if x2 is not None else (0, 0)
@@ -677,6 +709,9 @@ def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, grou
     if p0 is not None and (x2 is None or p1 is not None):
         # statistics came with the producing conv: only the per-(image, group) finalize runs
         ab = torch.empty((n, c, 2), dtype=torch.float32, device=x.device)
+        if defer and GN_PARTS_APPLY and h * w in GN_PARTS_APPLY_HW and x.dtype == torch.bfloat16 and groups <= 256:
+            ab._rdeic_pending = (p0, c0, p1, c1, n, h * w, groups, float(eps), gamma, beta)
+            return ab
         call("rdeic_groupnorm_parts_ab", p0.data_ptr(), c0, _ptr(p1), c1, n, h * w, groups, float(eps),
              gamma.data_ptr(), beta.data_ptr(), ab.data_ptr(), stream_ptr())
         return ab
@@ -691,6 +726,7 @@ def group_norm_ab(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, grou
 def group_norm_apply(x: torch.Tensor, ab: torch.Tensor, silu: bool, out: Optional[torch.Tensor] = None,
                      out_mul: float = 1.0) -> torch.Tensor:
     """y = silu?(x*a + b) * out_mul; `ab` may be a channel slice ab[:, c0:] of a wider affine."""
+    _ab_ready(ab)
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)

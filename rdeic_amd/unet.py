@@ -198,11 +198,11 @@ class UNet:
         """stats: the output feeds a GroupNorm (its statistics come fused with the last conv)."""
         s = self.store
         ab1 = ops.group_norm_ab(x, s.get(rb.prefix + ".in_layers.0.weight"), s.get(rb.prefix + ".in_layers.0.bias"),
-                                rb.gn_in, 1e-5, x2=x2)
+                                rb.gn_in, 1e-5, x2=x2, defer=True)
         h = ops.conv2d(x, s.conv(rb.prefix + ".in_layers.2"), x2=x2, gn=ab1, gn_silu=True,
                        emb=emb_all[:, rb.emb_off:rb.emb_off + rb.cout], stats=True)
         ab2 = ops.group_norm_ab(h, s.get(rb.prefix + ".out_layers.0.weight"),
-                                s.get(rb.prefix + ".out_layers.0.bias"), rb.gn_out, 1e-5)
+                                s.get(rb.prefix + ".out_layers.0.bias"), rb.gn_out, 1e-5, defer=True)
         if rb.cin != rb.cout:
             skip = ops.conv2d(x, s.conv(rb.prefix + ".skip_connection"), x2=x2)
         else:
@@ -218,7 +218,8 @@ class UNet:
         L = H * W_
         rows = B * L
         tb = t.prefix + ".transformer_blocks.0"
-        ab = ops.group_norm_ab(x, s.get(t.prefix + ".norm.weight"), s.get(t.prefix + ".norm.bias"), t.gn, 1e-6)
+        ab = ops.group_norm_ab(x, s.get(t.prefix + ".norm.weight"), s.get(t.prefix + ".norm.bias"), t.gn, 1e-6,
+                               defer=True)
         h4 = ops.conv2d(x, s.conv(t.prefix + ".proj_in"), gn=ab, gn_silu=False)
         h = h4.view(rows, C)
         scale = t.dh ** -0.5

@@ -91,3 +91,45 @@ def test_fused_stats_concat_linear_and_splitk(gpu):
     gamma, beta = _gamma_beta(1280)
     ab_f = ops.group_norm_ab(y, gamma, beta, 32, 1e-5)
     torch.testing.assert_close(ab_f, _standalone(y, gamma, beta, 32, 1e-5), rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("n,h,c0,c1,groups,silu", [(3, 16, 1280, 0, 32, True), (2, 8, 1280, 640, 32, True),
+                                                   (2, 16, 640, 640, 32, False), (4, 8, 320, 0, 16, True),
+                                                   (1, 16, 2560, 0, 32, True), (2, 8, 640, 1280, 32, True)])
+def test_parts_apply_bit_identical(gpu, n, h, c0, c1, groups, silu):
+    """rdeic_groupnorm_parts_apply (the UNet's 16^2 / 8^2 GroupNorms: finalize + apply in one launch, through
+    group_norm_ab(defer=True) -> conv2d(gn=...)) against the two-launch form (parts_ab, then the apply kernel):
+    the affine and the normalised conv input are bit-identical, including a skip concat whose groups straddle the
+    segments."""
+    from rdeic_amd import ops
+    xa = (torch.randn(n, h, h, 256, device="cuda") * 2 + 0.5).to(torch.bfloat16)
+    ya = ops.conv2d(xa, _conv(256, c0, seed=3), stats=True)
+    yb = ops.conv2d(xa, _conv(256, c1, seed=4), stats=True) if c1 else None
+    gamma, beta = _gamma_beta(c0 + c1, seed=7)
+    pc = _conv(c0 + c1, 128, k=1, seed=5)
+    c_before = ops.launch_count(ops.COUNT_GN_PARTS_APPLY)
+    ab_d = ops.group_norm_ab(ya, gamma, beta, groups, 1e-5, x2=yb, defer=True)
+    assert getattr(ab_d, "_rdeic_pending", None) is not None
+    out_d = ops.conv2d(ya, pc, x2=yb, gn=ab_d, gn_silu=silu)
+    torch.cuda.synchronize()
+    assert ops.launch_count(ops.COUNT_GN_PARTS_APPLY) == c_before + 1
+    assert getattr(ab_d, "_rdeic_pending", None) is None
+    ab_n = ops.group_norm_ab(ya, gamma, beta, groups, 1e-5, x2=yb)
+    out_n = ops.conv2d(ya, pc, x2=yb, gn=ab_n, gn_silu=silu)
+    torch.cuda.synchronize()
+    assert torch.equal(ab_d, ab_n)
+    assert torch.equal(out_d, out_n)
+
+
+def test_parts_apply_deferred_affine_finalized_for_other_consumers(gpu):
+    """A deferred affine read by anything but the materialised GroupNorm (here the apply kernel directly) is
+    finalized first."""
+    from rdeic_amd import ops
+    xa = torch.randn(2, 16, 16, 256, device="cuda").to(torch.bfloat16)
+    y = ops.conv2d(xa, _conv(256, 320, seed=9), stats=True)
+    gamma, beta = _gamma_beta(320, seed=2)
+    ab_d = ops.group_norm_ab(y, gamma, beta, 32, 1e-5, defer=True)
+    o_d = ops.group_norm_apply(y, ab_d, silu=True)
+    ab_n = ops.group_norm_ab(y, gamma, beta, 32, 1e-5)
+    o_n = ops.group_norm_apply(y, ab_n, silu=True)
+    assert torch.equal(ab_d, ab_n) and torch.equal(o_d, o_n)
