@@ -22,43 +22,43 @@ namespace {
 // No LDS staging of operands, no im2col. The MFMA sequence over k is conv_kernel's (k-steps 0..3 in order, zero
 // products included), so the accumulators equal the register tile's bit for bit.
 // The kernel is bound by its 1 GB of output stores, so its epilogue is WAVE-PRIVATE: each wave (64 pixels = one
-// canonical 64-row GroupNorm block x 64 channels) rounds its tile to bf16 into its own LDS region, then
-//   * stores it as 16-byte row chunks (8 lanes per 128-byte pixel row),
-//   * and scans it for the GroupNorm partials: lane (4-channel quad, 16-row group g) sums its group's rows in
+// canonical 64-row GroupNorm block x 32 channels) rounds its tile to bf16 into its own LDS region, then
+//   * stores it as 16-byte row chunks (4 lanes per 64-byte pixel row slice),
+//   * and scans it for the GroupNorm partials: lane (channel pair, 16-row group g) sums its group's rows in
 //     order (fmaf for the squares), and ((g0 + g1) + g2) + g3 is taken across the four lane quarters: the
 //     canonical order of epilogue_vec / gn_rows_partial, so the statistics are bit-identical too;
 // with no block barrier anywhere (epilogue_vec's four parked passes took 8 block barriers per 128 pixels).
 // ============================================================================================
-constexpr int CI_NT = 256;            // 4 waves: 2 pixel blocks of 64 x 2 channel halves of 64
-constexpr int CI_ROWB = 136;          // LDS bytes per parked pixel row (64 bf16 + 8): conflict-free scans
+constexpr int CI_NT = 512;            // 8 waves: 2 pixel blocks of 64 x 4 channel quarters of 32
+constexpr int CI_ROWB = 68;           // LDS bytes per parked pixel row (32 bf16 + 4): conflict-free scans
 constexpr int CI_WLDS = 64 * CI_ROWB; // per wave
 
-__global__ __launch_bounds__(CI_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv_in8_kernel(ConvArgs a, int tiles_n) {
+__global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int mt = blockIdx.x / tiles_n, nt = blockIdx.x - mt * tiles_n;
-  const int m0 = mt * 128 + (wave >> 1) * 64;  // this wave's 64 pixels
-  const int c0 = nt * 128 + (wave & 1) * 64;   // ... and 64 channels
-  if (c0 >= a.cout || m0 >= a.M) return;     // wave-uniform (cout % 64 == 0)
+  const int m0 = mt * 128 + (wave >> 2) * 64;  // this wave's 64 pixels
+  const int c0 = nt * 128 + (wave & 3) * 32;   // ... and 32 channels
+  if (c0 >= a.cout || m0 >= a.M) return;     // wave-uniform (cout % 32 == 0)
   char* const W = lds + wave * CI_WLDS;
   const int lr = lane & 15, lq = lane >> 4;
   const int hw = a.h * a.w;
   const bf16* wt = reinterpret_cast<const bf16*>(a.weight);
   const bf16* in = reinterpret_cast<const bf16*>(a.in0);
 
-  f32x4 acc[4][4];
+  // every operand load first (k-steps 0..2; step 2 holds only tap 8 / k 64..71, in the lq = 0 lanes; step 3 is
+  // the zero tail of the second 64-deep k-tile), then the MFMAs
+  bf16x8 bfv[3][2], af[3][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int s = 0; s < 3; ++s) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    bf16x8 bfv[4], af[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)  // k = 32 s + 8 lq of weight row c0 + 16 j + lr
-      bfv[j] = *reinterpret_cast<const bf16x8*>(wt + (long)(c0 + 16 * j + lr) * a.wld + 32 * s + 8 * lq);
-    const int tap = 4 * s + lq;  // this lane's k-chunk in k-step s; taps >= 9 are the zero tail
+    for (int j = 0; j < 2; ++j) {  // k = 32 s + 8 lq of weight row c0 + 16 j + lr
+      bf16x8 v = {};
+      if (s < 2 || lq == 0) v = *reinterpret_cast<const bf16x8*>(wt + (long)(c0 + 16 * j + lr) * a.wld + 32 * s + 8 * lq);
+      bfv[s][j] = v;
+    }
+    const int tap = 4 * s + lq;
     const int ky = tap / 3, kx = tap - (tap / 3) * 3;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -70,16 +70,26 @@ __global__ __launch_bounds__(CI_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
         if ((unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w)
           v = *reinterpret_cast<const bf16x8*>(in + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
       }
-      af[i] = v;
+      af[s][i] = v;
     }
+  }
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 zero = {};
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
-  }
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(s < 3 ? af[s < 3 ? s : 0][i] : zero,
+                                                             s < 3 ? bfv[s < 3 ? s : 0][j] : zero, acc[i][j], 0, 0, 0);
   // (acc + bias) rounded to bf16, parked row-major: lane holds channel 16 j + lr of pixels 16 i + 4 lq + r
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 2; ++j) {
     const float b = a.bias ? a.bias[c0 + 16 * j + lr] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -91,39 +101,37 @@ __global__ __launch_bounds__(CI_NT) __attribute__((amdgpu_waves_per_eu(4, 4))) v
   __builtin_amdgcn_wave_barrier();
   bf16* const out = reinterpret_cast<bf16*>(a.out);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {  // 8 lanes per pixel row: 16 bytes each
-    const int row = 8 * k + (lane >> 3), ch = lane & 7;
-    const uint2 lo = *reinterpret_cast<const uint2*>(W + row * CI_ROWB + ch * 16);
-    const uint2 hi = *reinterpret_cast<const uint2*>(W + row * CI_ROWB + ch * 16 + 8);
-    if (m0 + row < a.M) *reinterpret_cast<uint4*>(out + (long)(m0 + row) * a.out_ld + c0 + ch * 8) = uint4{lo.x, lo.y, hi.x, hi.y};
+  for (int k = 0; k < 4; ++k) {  // 4 lanes per pixel row of 64 bytes, 16 rows per instruction
+    const int row = 16 * k + (lane >> 2), ch = lane & 3;
+    const unsigned* src = reinterpret_cast<const unsigned*>(W + row * CI_ROWB + ch * 16);
+    const uint4 v = uint4{src[0], src[1], src[2], src[3]};
+    if (m0 + row < a.M) *reinterpret_cast<uint4*>(out + (long)(m0 + row) * a.out_ld + c0 + ch * 8) = v;
   }
   if (!a.gn_part) return;
-  const int q4 = lane & 15, g = lane >> 4;  // channels c0 + 4 q4 .. + 3, rows 16 g .. 16 g + 15
+  const int p2 = lane & 15, g = lane >> 4;  // channels c0 + 2 p2, + 1; rows 16 g .. 16 g + 15
   const int nv = a.M - (m0 + 16 * g);       // valid rows of the group
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const uint2 w2 = *reinterpret_cast<const uint2*>(W + (16 * g + r) * CI_ROWB + q4 * 8);
+    const unsigned w = *reinterpret_cast<const unsigned*>(W + (16 * g + r) * CI_ROWB + p2 * 4);
     if (r < nv) {
-      const float y[4] = {__uint_as_float(w2.x << 16), __uint_as_float(w2.x & 0xffff0000u), __uint_as_float(w2.y << 16),
-                          __uint_as_float(w2.y & 0xffff0000u)};
+      const float y[2] = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < 2; ++e) {
         s1[e] += y[e];
         s2[e] = fmaf(y[e], y[e], s2[e]);
       }
     }
   }
-  float t1[4], t2[4];
+  float t1[2], t2[2];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {  // ((g0 + g1) + g2) + g3 in the quarter-0 lanes
-    t1[e] = ((s1[e] + __shfl(s1[e], q4 + 16, 64)) + __shfl(s1[e], q4 + 32, 64)) + __shfl(s1[e], q4 + 48, 64);
-    t2[e] = ((s2[e] + __shfl(s2[e], q4 + 16, 64)) + __shfl(s2[e], q4 + 32, 64)) + __shfl(s2[e], q4 + 48, 64);
+  for (int e = 0; e < 2; ++e) {  // ((g0 + g1) + g2) + g3 in the quarter-0 lanes
+    t1[e] = ((s1[e] + __shfl(s1[e], p2 + 16, 64)) + __shfl(s1[e], p2 + 32, 64)) + __shfl(s1[e], p2 + 48, 64);
+    t2[e] = ((s2[e] + __shfl(s2[e], p2 + 16, 64)) + __shfl(s2[e], p2 + 32, 64)) + __shfl(s2[e], p2 + 48, 64);
   }
   if (g == 0) {
-    float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0) / 64) * a.cout + c0 + 4 * q4) * 2;
+    float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0) / 64) * a.cout + c0 + 2 * p2) * 2;
     *reinterpret_cast<float4*>(pp) = make_float4(t1[0], t2[0], t1[1], t2[1]);
-    *reinterpret_cast<float4*>(pp + 4) = make_float4(t1[2], t2[2], t1[3], t2[3]);
     if (lane == 0 && m0 == 0 && c0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
   }
 }
@@ -151,7 +159,8 @@ template <int TR> struct Narrow {
 __device__ __forceinline__ int nr_sw(int s) { return ((s >> 2) & 1) << 1; }  // halo conv swizzle (conflict-free)
 
 template <int TR, bool SILU>
-__global__ __launch_bounds__(TR * 64) void conv3x3_gn_narrow_kernel(ConvArgs a, int tiles_x, int tiles_y) {
+__global__ __launch_bounds__(TR * 64) __attribute__((amdgpu_waves_per_eu(4, 4))) void conv3x3_gn_narrow_kernel(
+    ConvArgs a, int tiles_x, int tiles_y) {
   using NR = Narrow<TR>;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* const abl = reinterpret_cast<float*>(lds + NR::LDS);  // the image's GroupNorm (a, b) table
@@ -171,23 +180,29 @@ __global__ __launch_bounds__(TR * 64) void conv3x3_gn_narrow_kernel(ConvArgs a, 
 
   for (int i = tid; i < cin / 2; i += NR::NT)
     reinterpret_cast<float4*>(abl)[i] = reinterpret_cast<const float4*>(a.gn_ab + (long)img * cin * 2)[i];
-  uint4 raw[NR::IPT];
-  auto load = [&](int cb) {  // the raw halo chunks of this thread (zeros outside the image)
+  // per item: the chunk's element offset in the input (-1: outside the image / past the halo) and its LDS slot,
+  // the same for every channel block (computed once)
+  int goff[NR::IPT], loff[NR::IPT];
 #pragma unroll
-    for (int k = 0; k < NR::IPT; ++k) {
-      const int it = tid + k * NR::NT, hp = it >> 2;
-      const int hr = hp / NR_HC, hc = hp - (hp / NR_HC) * NR_HC;
-      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
-      raw[k] = uint4{0u, 0u, 0u, 0u};
-      if (it < NR::ITEMS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-        raw[k] = *reinterpret_cast<const uint4*>(in + ((long)(img * H + iy) * W + ix) * a.ld0 + cb + 8 * q);
-    }
+  for (int k = 0; k < NR::IPT; ++k) {
+    const int it = tid + k * NR::NT, hp = it >> 2;
+    const int hr = hp / NR_HC, hc = hp - (hp / NR_HC) * NR_HC;
+    const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
+    goff[k] = (it < NR::ITEMS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                  ? ((img * H + iy) * W + ix) * a.ld0 + 8 * q : -1;
+    loff[k] = it < NR::ITEMS ? hp * 64 + ((q ^ nr_sw(hp)) << 4) : -1;
+  }
+  uint4 raw[NR::IPT];
+  auto load = [&](int cb, int k) {  // raw halo chunk k of this thread (zeros outside the image)
+    raw[k] = uint4{0u, 0u, 0u, 0u};
+    if (goff[k] >= 0) raw[k] = *reinterpret_cast<const uint4*>(in + goff[k] + cb);
   };
   f32x4 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load(0);
+#pragma unroll
+  for (int k = 0; k < NR::IPT; ++k) load(0, k);
   for (int cb = 0; cb < cin; cb += 32) {
     bar();  // cb = 0: the (a, b) table is in LDS; else the previous block's MFMA reads of the halo are done
     const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb + 8 * q) * 2);
@@ -196,12 +211,8 @@ __global__ __launch_bounds__(TR * 64) void conv3x3_gn_narrow_kernel(ConvArgs a, 
     const f32x2 bv[4] = {{t0.y, t0.w}, {t1.y, t1.w}, {t2.y, t2.w}, {t3.y, t3.w}};
 #pragma unroll
     for (int k = 0; k < NR::IPT; ++k) {
-      const int it = tid + k * NR::NT, hp = it >> 2;
-      if (it >= NR::ITEMS) continue;
-      const int hr = hp / NR_HC, hc = hp - (hp / NR_HC) * NR_HC;
-      const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
       uint4 o = uint4{0u, 0u, 0u, 0u};
-      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {  // outside: the normalised tensor's zero pad
+      if (goff[k] >= 0) {  // outside: the normalised tensor's zero pad
         const unsigned w4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
         unsigned o4[4];
 #pragma unroll
@@ -216,10 +227,10 @@ __global__ __launch_bounds__(TR * 64) void conv3x3_gn_narrow_kernel(ConvArgs a, 
         }
         o = uint4{o4[0], o4[1], o4[2], o4[3]};
       }
-      *reinterpret_cast<uint4*>(lds + hp * 64 + ((q ^ nr_sw(hp)) << 4)) = o;
+      if (loff[k] >= 0) *reinterpret_cast<uint4*>(lds + loff[k]) = o;
+      if (cb + 32 < cin) load(cb + 32, k);  // the next block's chunk flies under the rest of this block's work
     }
     bar();
-    if (cb + 32 < cin) load(cb + 32);  // the next block's loads fly under this block's MFMAs
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int ky = t / 3, kx = t - (t / 3) * 3;
@@ -262,7 +273,7 @@ int launch_edge(const rdeic_conv_desc* d, const ConvArgs& a, hipStream_t s, bool
       ((uintptr_t)d->in0) % 16 || ((uintptr_t)d->weight) % 16)
     return -1;
   // conv_in: 8 input channels, bias only, bf16 output, statistics per image (64-row blocks)
-  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout % 64 == 0 && !d->emb && !d->act && !d->res &&
+  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout % 32 == 0 && !d->emb && !d->act && !d->res &&
       !d->out_f32 && !d->ln_rows && d->out_ld % 8 == 0 && ((uintptr_t)d->out) % 16 == 0) {
     ConvArgs e = a;
     const bool stats = e.gn_part != nullptr && e.gn_hw > 0 && e.gn_hw % 64 == 0;
@@ -271,7 +282,7 @@ int launch_edge(const rdeic_conv_desc* d, const ConvArgs& a, hipStream_t s, bool
     rdeic_count_launch(RDEIC_COUNT_EDGE);
     const int tn = (e.cout + 127) / 128;
     const long blocks = (long)((e.M + 127) / 128) * tn;
-    hipLaunchKernelGGL(conv_in8_kernel, dim3((unsigned)blocks), dim3(CI_NT), 4 * CI_WLDS, s, e, tn);
+    hipLaunchKernelGGL(conv_in8_kernel, dim3((unsigned)blocks), dim3(CI_NT), 8 * CI_WLDS, s, e, tn);
     return launch_status();
   }
   // norm -> (SiLU) -> conv to <= 16 channels
