@@ -243,7 +243,8 @@ def main():
             rf_elapsed = time.perf_counter() - tr0
             ops.prof_stop()
             prof = ops.prof_read()
-            prof = dict(prof, _wall_s=rf_elapsed)
+            prof = dict(prof, _wall_s=rf_elapsed,
+                        _attn_shapes={k: ops.prof_read_keys(k) for k in ("attention", "attention_dh16", "attention_d512")})
         elapsed = parallel.max_over_ranks(elapsed, dev)
         mrows = metrics.cpu().numpy()
         last_out = sessions[(args.steps - 1) % nsess]._last_out
@@ -339,6 +340,17 @@ def main():
                 sec[kind] = {"bound": "hbm", "achieved": round(a, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": round(a / PEAK_HBM_GBS, 4), "launches_per_step": round(cnt / args.steps, 1),
                              "ms_per_step": round(kms / args.steps, 3)}
+        # per-shape attribution of the attention kinds (self vs cross: lk == 77 is the text context)
+        shapes = []
+        for kind, rows in prof.get("_attn_shapes", {}).items():
+            for key, cnt, work, kms in rows:
+                if kms <= 0:
+                    continue
+                a = work / (kms * 1e-3) / 1e12
+                sh = ops.attention_key(key)
+                shapes.append(dict(kind=kind, **sh, cross=sh["lk"] != sh["lq"], launches_per_step=round(cnt / args.steps, 2),
+                                   ms_per_step=round(kms / args.steps, 4), achieved=round(a, 1), frac=round(a / peak, 4)))
+        sec["attention_by_shape"] = sorted(shapes, key=lambda r: -r["ms_per_step"])
         roof["secondary"] = sec
     cpu = None
     if world > 1:

@@ -341,6 +341,10 @@ int rdeic_ac_uniform_cdf(int32_t codebook_size, int16_t* cdf_row);
 #define RDEIC_PROF_CONV_BYTES 7  /* every conv launch (not sampled, no events): algorithmic HBM bytes — input
                                     (each element once), packed weight, output, residual — ms reads 0 */
 int rdeic_prof_start(int32_t capacity, int32_t every);
+/* Per-shape totals of one kind since rdeic_prof_start: up to cap distinct launch-shape keys (attention: dh << 48 |
+ * lq << 32 | lk << 16 | batch x heads, 16 bits each) with their weighted launches, work and event ms; returns the
+ * number written (synchronizes). */
+int rdeic_prof_read_keys(int32_t kind, int64_t* keys, int64_t* launches, double* work, double* ms, int32_t cap);
 /* Launch counters (always on, one relaxed atomic add per launch): which kernel a dispatcher chose,
  * so tests can assert that a fused path actually ran (e.g. the halo conv, not its fallback). */
 #define RDEIC_COUNT_HALO_CONV 0    /* conv3x3_halo_kernel (GroupNorm-input 3x3 convs, VAE geometry) */

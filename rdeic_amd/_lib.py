@@ -78,6 +78,8 @@ PROTOTYPES = {
     "rdeic_launch_count_reset": (C.c_int, []),
     "rdeic_layernorm_rowstats": (C.c_int, [C.c_void_p, _i32, _i32, _i32, C.c_float, C.c_void_p, C.c_void_p]),
     "rdeic_prof_read": (C.c_int, [_i32, C.POINTER(C.c_int64), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "rdeic_prof_read_keys": (C.c_int, [_i32, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                                       C.POINTER(C.c_double), _i32]),
     "rdeic_groupnorm_ws_floats": (_sz, [_i32, _i32, _i32]),
     "rdeic_groupnorm_stats": (C.c_int, [_p, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p,
                                         _i32, _p]),

@@ -1438,8 +1438,11 @@ extern "C" int rdeic_attention(const void* q, int32_t ldq, const void* k, int32_
   if (ldq % epc || ldk % epc || ldv % epc || ((uintptr_t)k) % 16 || ((uintptr_t)v) % 16 || ((uintptr_t)q) % 16)
     return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  // shape tag for the per-shape read-out (rdeic_prof_read_keys): dh, lq, lk, batch x heads (16 bits each)
+  const long long key = ((long long)(dh & 0xffff) << 48) | ((long long)(lq < 0xffff ? lq : 0xffff) << 32) |
+                        ((long long)(lk < 0xffff ? lk : 0xffff) << 16) | (batch * heads < 0xffff ? batch * heads : 0xffff);
   ProfScope ps(s, dh == 512 ? RDEIC_PROF_ATTN_D512 : dh >= 64 ? RDEIC_PROF_ATTN : RDEIC_PROF_ATTN_SMALL,
-               4.0 * batch * heads * (double)lq * lk * dh);
+               4.0 * batch * heads * (double)lq * lk * dh, key);
   if (dtype == 1) return launch_attn<bf16>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
   return launch_attn<float>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, dh, scale, kv_bcast, s);
 }

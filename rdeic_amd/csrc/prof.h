@@ -9,11 +9,12 @@ void rdeic_count_launch(int kind);  // RDEIC_COUNT_* (include/rdeic_hip.h): whic
 
 void rdeic_prof_add_bytes(double bytes);  // RDEIC_PROF_CONV_BYTES accumulator (no-op when profiling is off)
 int rdeic_prof_begin(hipStream_t s, int kind, double work);           // slot, or -1 (off / full / not sampled)
-void rdeic_prof_end(int slot, hipStream_t s, int kind, double work);  // no-op for slot < 0
+void rdeic_prof_end(int slot, hipStream_t s, int kind, double work, long long key = 0);  // no-op for slot < 0
 
+// key: an optional launch-shape tag (rdeic_prof_read_keys aggregates per (kind, key))
 struct ProfScope {
-  int slot; hipStream_t s; int kind; double work;
-  ProfScope(hipStream_t s_, int kind_, double work_)
-      : slot(rdeic_prof_begin(s_, kind_, work_)), s(s_), kind(kind_), work(work_) {}
-  ~ProfScope() { rdeic_prof_end(slot, s, kind, work); }
+  int slot; hipStream_t s; int kind; double work; long long key;
+  ProfScope(hipStream_t s_, int kind_, double work_, long long key_ = 0)
+      : slot(rdeic_prof_begin(s_, kind_, work_)), s(s_), kind(kind_), work(work_), key(key_) {}
+  ~ProfScope() { rdeic_prof_end(slot, s, kind, work, key); }
 };

@@ -30,7 +30,7 @@ extern "C" int rdeic_launch_count_reset(void) {
 }
 
 namespace {
-struct Slot { hipEvent_t a = nullptr, b = nullptr; int kind = -1; double work = 0.0; double weight = 1.0; };
+struct Slot { hipEvent_t a = nullptr, b = nullptr; int kind = -1; double work = 0.0; double weight = 1.0; long long key = 0; };
 std::vector<Slot> g_slots;
 int g_used = 0;
 bool g_on = false;
@@ -75,12 +75,13 @@ void rdeic_prof_add_bytes(double bytes) {
   g_bytes += bytes;
 }
 
-void rdeic_prof_end(int slot, hipStream_t s, int kind, double work) {
+void rdeic_prof_end(int slot, hipStream_t s, int kind, double work, long long key) {
   if (slot < 0) return;
   std::lock_guard<std::mutex> lk(g_mu);
   if (hipEventRecord(g_slots[slot].b, s) != hipSuccess) return;
   g_slots[slot].kind = kind;
   g_slots[slot].work = work;
+  g_slots[slot].key = key;
 }
 
 extern "C" int rdeic_prof_start(int32_t capacity, int32_t every) {
@@ -128,4 +129,28 @@ extern "C" int rdeic_prof_read(int32_t kind, int64_t* launches, double* work, do
   }
   *launches = (int64_t)(n + 0.5); *work = w; *ms = t_ms;
   return RDEIC_OK;
+}
+
+extern "C" int rdeic_prof_read_keys(int32_t kind, int64_t* keys, int64_t* launches, double* work, double* ms,
+                                    int32_t cap) {
+  if (!keys || !launches || !work || !ms || cap <= 0) return RDEIC_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::vector<long long> ks;
+  std::vector<double> n, w, t;
+  for (int i = 0; i < g_used; ++i) {
+    const Slot& sl = g_slots[i];
+    if (sl.kind != kind) continue;
+    if (hipEventSynchronize(sl.b) != hipSuccess) return RDEIC_ELAUNCH;
+    float e = 0.f;
+    if (hipEventElapsedTime(&e, sl.a, sl.b) != hipSuccess) return RDEIC_ELAUNCH;
+    size_t j = 0;
+    while (j < ks.size() && ks[j] != sl.key) ++j;
+    if (j == ks.size()) { ks.push_back(sl.key); n.push_back(0.0); w.push_back(0.0); t.push_back(0.0); }
+    n[j] += sl.weight; w[j] += sl.weight * sl.work; t[j] += sl.weight * e;
+  }
+  const int m = (int)ks.size() < cap ? (int)ks.size() : cap;
+  for (int j = 0; j < m; ++j) {
+    keys[j] = ks[j]; launches[j] = (int64_t)(n[j] + 0.5); work[j] = w[j]; ms[j] = t[j];
+  }
+  return m;
 }

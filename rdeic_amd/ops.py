@@ -475,6 +475,19 @@ def prof_read() -> dict:
     return out
 
 
+def prof_read_keys(kind: str, cap: int = 64) -> list:
+    """[(key, launches, work, event ms)] per launch-shape key of one kind (rdeic_prof_read_keys; synchronizes)."""
+    keys, n = (C.c_int64 * cap)(), (C.c_int64 * cap)()
+    w, ms = (C.c_double * cap)(), (C.c_double * cap)()
+    m = int(_lib.load().rdeic_prof_read_keys(PROF_KINDS[kind], keys, n, w, ms, cap))
+    return [(int(keys[i]), int(n[i]), float(w[i]), float(ms[i])) for i in range(max(0, m))]
+
+
+def attention_key(key: int) -> dict:
+    """Decode an attention profiler key: head dim, query / key lengths, batch x heads."""
+    return {"dh": (key >> 48) & 0xffff, "lq": (key >> 32) & 0xffff, "lk": (key >> 16) & 0xffff, "bh": key & 0xffff}
+
+
 def other_profile_summary():
     """{kind: (launches, total work, total ms)} of the secondary kernels (after sync)."""
     out = {}
