@@ -29,110 +29,126 @@ namespace {
 //     canonical order of epilogue_vec / gn_rows_partial, so the statistics are bit-identical too;
 // with no block barrier anywhere (epilogue_vec's four parked passes took 8 block barriers per 128 pixels).
 // ============================================================================================
-constexpr int CI_NT = 512;            // 8 waves: 2 pixel blocks of 64 x 4 channel quarters of 32
+constexpr int CI_NT = 256;            // 4 waves: one 64-pixel block x 4 channel quarters of 32
 constexpr int CI_ROWB = 68;           // LDS bytes per parked pixel row (32 bf16 + 4): conflict-free scans
 constexpr int CI_WLDS = 64 * CI_ROWB; // per wave
 
-__global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int tiles_n) {
+// Persistent: block b takes the 64-pixel tiles b, b + grid, ... (all cout <= 128 channels each); every wave
+// issues the next tile's A loads right after its MFMAs consumed the current ones, so they fly under the epilogue.
+// ~150 VGPRs: three 4-wave blocks per CU.
+__global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mt = blockIdx.x / tiles_n, nt = blockIdx.x - mt * tiles_n;
-  const int m0 = mt * 128 + (wave >> 2) * 64;  // this wave's 64 pixels
-  const int c0 = nt * 128 + (wave & 3) * 32;   // ... and 32 channels
-  if (c0 >= a.cout || m0 >= a.M) return;     // wave-uniform (cout % 32 == 0)
+  const int c0 = (wave & 3) * 32;  // this wave's 32 channels
+  if (c0 >= a.cout) return;        // wave-uniform (cout % 32 == 0, <= 128)
   char* const W = lds + wave * CI_WLDS;
   const int lr = lane & 15, lq = lane >> 4;
   const int hw = a.h * a.w;
   const bf16* wt = reinterpret_cast<const bf16*>(a.weight);
   const bf16* in = reinterpret_cast<const bf16*>(a.in0);
+  bf16* const out = reinterpret_cast<bf16*>(a.out);
 
-  // every operand load first (k-steps 0..2; step 2 holds only tap 8 / k 64..71, in the lq = 0 lanes; step 3 is
-  // the zero tail of the second 64-deep k-tile), then the MFMAs
-  bf16x8 bfv[3][2], af[3][4];
+  // B fragments (k-steps 0..2; step 2 holds only k 64..71, in the lq = 0 lanes): the same for every tile
+  bf16x8 bfv[3][2];
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
+  for (int s = 0; s < 3; ++s)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {  // k = 32 s + 8 lq of weight row c0 + 16 j + lr
       bf16x8 v = {};
       if (s < 2 || lq == 0) v = *reinterpret_cast<const bf16x8*>(wt + (long)(c0 + 16 * j + lr) * a.wld + 32 * s + 8 * lq);
       bfv[s][j] = v;
     }
-    const int tap = 4 * s + lq;
-    const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+  float bias[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + i * 16 + lr;
-      bf16x8 v = {};
-      if (tap < 9 && m < a.M) {
-        const int img = m / hw, rem = m - img * hw;
-        const int iy = rem / a.w + ky - 1, ix = rem - (rem / a.w) * a.w + kx - 1;
-        if ((unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w)
-          v = *reinterpret_cast<const bf16x8*>(in + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
+  for (int j = 0; j < 2; ++j) bias[j] = a.bias ? a.bias[c0 + 16 * j + lr] : 0.f;
+  bf16x8 af[3][4];
+  auto load_a = [&](int m0) {  // A fragments of the 64 pixels from m0 (one 16-byte pixel load per tap)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int tap = 4 * s + lq;
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + i * 16 + lr;
+        bf16x8 v = {};
+        if (tap < 9 && m < a.M) {
+          const int img = m / hw, rem = m - img * hw;
+          const int iy = rem / a.w + ky - 1, ix = rem - (rem / a.w) * a.w + kx - 1;
+          if ((unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w)
+            v = *reinterpret_cast<const bf16x8*>(in + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
+        }
+        af[s][i] = v;
       }
-      af[s][i] = v;
     }
-  }
-  f32x4 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16x8 zero = {};
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) load_a(t * 64);
+  for (; t < ntiles; t += gridDim.x) {
+    const int m0 = t * 64;  // this wave's 64 pixels
+    f32x4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(s < 3 ? af[s < 3 ? s : 0][i] : zero,
-                                                             s < 3 ? bfv[s < 3 ? s : 0][j] : zero, acc[i][j], 0, 0, 0);
-  // (acc + bias) rounded to bf16, parked row-major: lane holds channel 16 j + lr of pixels 16 i + 4 lq + r
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16x8 zero = {};
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const float b = a.bias ? a.bias[c0 + 16 * j + lr] : 0.f;
+    for (int s = 0; s < 4; ++s)  // k-step 3 is the zero tail of the second 64-deep k-tile (conv_kernel's order)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        *reinterpret_cast<bf16*>(W + (16 * i + 4 * lq + r) * CI_ROWB + (16 * j + lr) * 2) = (bf16)(acc[i][j][r] + b);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS tile, written by all its lanes
-  __builtin_amdgcn_wave_barrier();
-  bf16* const out = reinterpret_cast<bf16*>(a.out);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(s < 3 ? af[s < 3 ? s : 0][i] : zero,
+                                                               s < 3 ? bfv[s < 3 ? s : 0][j] : zero, acc[i][j], 0, 0, 0);
+    if (t + (int)gridDim.x < ntiles) load_a((t + gridDim.x) * 64);  // under the epilogue
+    // the previous tile's LDS reads of this wave are done before its tile is overwritten
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // (acc + bias) rounded to bf16, parked row-major: lane holds channel 16 j + lr of pixels 16 i + 4 lq + r
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {  // 4 lanes per pixel row of 64 bytes, 16 rows per instruction
-    const int row = 16 * k + (lane >> 2), ch = lane & 3;
-    const unsigned* src = reinterpret_cast<const unsigned*>(W + row * CI_ROWB + ch * 16);
-    const uint4 v = uint4{src[0], src[1], src[2], src[3]};
-    if (m0 + row < a.M) *reinterpret_cast<uint4*>(out + (long)(m0 + row) * a.out_ld + c0 + ch * 8) = v;
-  }
-  if (!a.gn_part) return;
-  const int p2 = lane & 15, g = lane >> 4;  // channels c0 + 2 p2, + 1; rows 16 g .. 16 g + 15
-  const int nv = a.M - (m0 + 16 * g);       // valid rows of the group
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const unsigned w = *reinterpret_cast<const unsigned*>(W + (16 * g + r) * CI_ROWB + p2 * 4);
-    if (r < nv) {
-      const float y[2] = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        s1[e] += y[e];
-        s2[e] = fmaf(y[e], y[e], s2[e]);
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<bf16*>(W + (16 * i + 4 * lq + r) * CI_ROWB + (16 * j + lr) * 2) = (bf16)(acc[i][j][r] + bias[j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS tile, written by all its lanes
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // 4 lanes per pixel row of 64 bytes, 16 rows per instruction
+      const int row = 16 * k + (lane >> 2), ch = lane & 3;
+      const unsigned* src = reinterpret_cast<const unsigned*>(W + row * CI_ROWB + ch * 16);
+      const uint4 v = uint4{src[0], src[1], src[2], src[3]};
+      if (m0 + row < a.M) *reinterpret_cast<uint4*>(out + (long)(m0 + row) * a.out_ld + c0 + ch * 8) = v;
+    }
+    if (a.gn_part) {
+      const int p2 = lane & 15, g = lane >> 4;  // channels c0 + 2 p2, + 1; rows 16 g .. 16 g + 15
+      const int nv = a.M - (m0 + 16 * g);       // valid rows of the group
+      float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned w = *reinterpret_cast<const unsigned*>(W + (16 * g + r) * CI_ROWB + p2 * 4);
+        if (r < nv) {
+          const float y[2] = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            s1[e] += y[e];
+            s2[e] = fmaf(y[e], y[e], s2[e]);
+          }
+        }
+      }
+      float t1[2], t2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {  // ((g0 + g1) + g2) + g3 in the quarter-0 lanes
+        t1[e] = ((s1[e] + __shfl(s1[e], p2 + 16, 64)) + __shfl(s1[e], p2 + 32, 64)) + __shfl(s1[e], p2 + 48, 64);
+        t2[e] = ((s2[e] + __shfl(s2[e], p2 + 16, 64)) + __shfl(s2[e], p2 + 32, 64)) + __shfl(s2[e], p2 + 48, 64);
+      }
+      if (g == 0 && m0 < a.M) {
+        float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0) / 64) * a.cout + c0 + 2 * p2) * 2;
+        *reinterpret_cast<float4*>(pp) = make_float4(t1[0], t2[0], t1[1], t2[1]);
+        if (lane == 0 && m0 == 0 && c0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
       }
     }
-  }
-  float t1[2], t2[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {  // ((g0 + g1) + g2) + g3 in the quarter-0 lanes
-    t1[e] = ((s1[e] + __shfl(s1[e], p2 + 16, 64)) + __shfl(s1[e], p2 + 32, 64)) + __shfl(s1[e], p2 + 48, 64);
-    t2[e] = ((s2[e] + __shfl(s2[e], p2 + 16, 64)) + __shfl(s2[e], p2 + 32, 64)) + __shfl(s2[e], p2 + 48, 64);
-  }
-  if (g == 0) {
-    float* pp = a.gn_part + 4 + ((long)((a.gn_row0 + m0) / 64) * a.cout + c0 + 2 * p2) * 2;
-    *reinterpret_cast<float4*>(pp) = make_float4(t1[0], t2[0], t1[1], t2[1]);
-    if (lane == 0 && m0 == 0 && c0 == 0) reinterpret_cast<int*>(a.gn_part)[0] = 64;  // rows per partial
   }
 }
 
@@ -175,7 +191,7 @@ __global__ __launch_bounds__(TR * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
   const int lr = lane & 15, lq = lane >> 4;
   const int q = tid & 3;  // this thread's 16-byte chunk of every halo pixel it loads (NT % 4 == 0)
   const bf16* in = reinterpret_cast<const bf16*>(a.in0);
-  // LDS-only barrier: __syncthreads() would also wait for the next channel block's loads in flight
+  // LDS-only barrier: __syncthreads() would also wait for the channel blocks' loads in flight
   auto bar = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
 
   for (int i = tid; i < cin / 2; i += NR::NT)
@@ -192,27 +208,27 @@ __global__ __launch_bounds__(TR * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
                   ? ((img * H + iy) * W + ix) * a.ld0 + 8 * q : -1;
     loff[k] = it < NR::ITEMS ? hp * 64 + ((q ^ nr_sw(hp)) << 4) : -1;
   }
-  uint4 raw[NR::IPT];
-  auto load = [&](int cb, int k) {  // raw halo chunk k of this thread (zeros outside the image)
+  // raw chunks of two channel blocks in flight (the HBM latency is ~2 blocks of transform + MFMA)
+  uint4 raw0[NR::IPT], raw1[NR::IPT];
+  auto load = [&](uint4 (&raw)[NR::IPT], int cb, int k) {
     raw[k] = uint4{0u, 0u, 0u, 0u};
-    if (goff[k] >= 0) raw[k] = *reinterpret_cast<const uint4*>(in + goff[k] + cb);
+    if (goff[k] >= 0 && cb < cin) raw[k] = *reinterpret_cast<const uint4*>(in + goff[k] + cb);
   };
   f32x4 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int k = 0; k < NR::IPT; ++k) load(0, k);
-  for (int cb = 0; cb < cin; cb += 32) {
-    bar();  // cb = 0: the (a, b) table is in LDS; else the previous block's MFMA reads of the halo are done
-    const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb + 8 * q) * 2);
-    const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
-    const f32x2 av[4] = {{t0.x, t0.z}, {t1.x, t1.z}, {t2.x, t2.z}, {t3.x, t3.z}};
-    const f32x2 bv[4] = {{t0.y, t0.w}, {t1.y, t1.w}, {t2.y, t2.w}, {t3.y, t3.w}};
+  // one channel block: transform its raw chunks into the halo (reloading the registers with block cb + 64), then
+  // the 9 taps
+  auto step = [&](uint4 (&raw)[NR::IPT], int cb) {
+    bar();  // the (a, b) table is in LDS / the previous block's MFMA reads of the halo are done
 #pragma unroll
     for (int k = 0; k < NR::IPT; ++k) {
       uint4 o = uint4{0u, 0u, 0u, 0u};
       if (goff[k] >= 0) {  // outside: the normalised tensor's zero pad
+        const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb + 8 * q) * 2);
+        const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
+        const f32x2 av[4] = {{t0.x, t0.z}, {t1.x, t1.z}, {t2.x, t2.z}, {t3.x, t3.z}};
+        const f32x2 bv[4] = {{t0.y, t0.w}, {t1.y, t1.w}, {t2.y, t2.w}, {t3.y, t3.w}};
         const unsigned w4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
         unsigned o4[4];
 #pragma unroll
@@ -228,22 +244,30 @@ __global__ __launch_bounds__(TR * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
         o = uint4{o4[0], o4[1], o4[2], o4[3]};
       }
       if (loff[k] >= 0) *reinterpret_cast<uint4*>(lds + loff[k]) = o;
-      if (cb + 32 < cin) load(cb + 32, k);  // the next block's chunk flies under the rest of this block's work
+      load(raw, cb + 64, k);  // two blocks ahead
     }
     bar();
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int ky = t / 3, kx = t - (t / 3) * 3;
+      // per-tap addresses from laundered bases (hoisted, the 36 fragment addresses would spill)
+      int lb = wave * NR_HC + lr, wb = lr * a.wld + cb + 8 * lq;
+      asm volatile("" : "+v"(lb), "+v"(wb));
       bf16x8 bfv = {};
-      if (lr < a.cout)
-        bfv = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.weight) + (long)lr * a.wld + t * cin + cb + 8 * lq);
+      if (lr < a.cout) bfv = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.weight) + wb + t * cin);
+      const int hp0 = lb + ky * NR_HC + kx;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int hp = (wave + ky) * NR_HC + i * 16 + lr + kx;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(lds + hp * 64 + ((lq ^ nr_sw(hp)) << 4));
+      for (int i = 0; i < 4; ++i) {  // + 16 i keeps the swizzle (bits 2 of the pixel index unchanged)
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(lds + (hp0 + 16 * i) * 64 + ((lq ^ nr_sw(hp0)) << 4));
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv, acc[i], 0, 0, 0);
       }
     }
+  };
+#pragma unroll
+  for (int k = 0; k < NR::IPT; ++k) { load(raw0, 0, k); load(raw1, 32, k); }
+  for (int cb = 0; cb < cin; cb += 64) {
+    step(raw0, cb);
+    if (cb + 32 < cin) step(raw1, cb + 32);
   }
   // lane: output channel lr, pixels ox0 + 16 i + 4 lq + r of row oy0 + wave
   if (lr >= a.cout) return;
@@ -273,20 +297,27 @@ int launch_edge(const rdeic_conv_desc* d, const ConvArgs& a, hipStream_t s, bool
       ((uintptr_t)d->in0) % 16 || ((uintptr_t)d->weight) % 16)
     return -1;
   // conv_in: 8 input channels, bias only, bf16 output, statistics per image (64-row blocks)
-  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout % 32 == 0 && !d->emb && !d->act && !d->res &&
+  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout % 32 == 0 && d->cout <= 128 && !d->emb && !d->act && !d->res &&
       !d->out_f32 && !d->ln_rows && d->out_ld % 8 == 0 && ((uintptr_t)d->out) % 16 == 0) {
     ConvArgs e = a;
     const bool stats = e.gn_part != nullptr && e.gn_hw > 0 && e.gn_hw % 64 == 0;
     if (!stats) e.gn_part = nullptr;
     if (fused) *fused = stats;
     rdeic_count_launch(RDEIC_COUNT_EDGE);
-    const int tn = (e.cout + 127) / 128;
-    const long blocks = (long)((e.M + 127) / 128) * tn;
-    hipLaunchKernelGGL(conv_in8_kernel, dim3((unsigned)blocks), dim3(CI_NT), 8 * CI_WLDS, s, e, tn);
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus <= 0)
+        cus = 256;
+    }
+    const int ntiles = (e.M + 63) / 64;
+    const int blocks = ntiles < 3 * cus ? ntiles : 3 * cus;  // three 4-wave blocks per CU
+    hipLaunchKernelGGL(conv_in8_kernel, dim3((unsigned)blocks), dim3(CI_NT), 4 * CI_WLDS, s, e, ntiles);
     return launch_status();
   }
   // norm -> (SiLU) -> conv to <= 16 channels
-  constexpr int TR = 8;
+  constexpr int TR = 16;
   if (d->gn_ab && d->cout <= 16 && d->c0 % 32 == 0 && d->c0 <= NR_AB_MAX && d->h % TR == 0 && d->w % NR_TC == 0 &&
       !d->gn_part && !d->emb && ((uintptr_t)d->gn_ab) % 16 == 0) {
     rdeic_count_launch(RDEIC_COUNT_EDGE);

@@ -26,7 +26,7 @@ FAMILIES = [  # (family, substring on the demangled name), first match wins
     ("conv", "conv3x3_halo"),
     ("conv", "conv_out_dot2"),
     ("attention", "attn"), ("vae_attention_softmax", "softmax_rows"),
-    ("groupnorm", "gn_"), ("layernorm", "layernorm"),
+    ("conv", "gn_narrow"), ("conv", "conv_in8"), ("groupnorm", "gn_"), ("layernorm", "layernorm"),
     ("entropy", "ckbd_"), ("entropy", "vq_argmin"), ("entropy", "gather_rows"), ("entropy", "row_sqnorm"),
     ("sampler", "ddim_step"), ("sampler", "spaced_step"), ("sampler", "axpby"), ("sampler", "cfg_combine"),
     ("image_io", "img_to_nhwc"), ("image_io", "nhwc_to_img"), ("image_io", "image_mse"),
