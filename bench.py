@@ -55,7 +55,10 @@ def conv_traffic(workload: dict):
 
 
 def parse(argv=None):
-    ap = argparse.ArgumentParser()
+    ap = argparse.ArgumentParser(epilog="environment: RDEIC_CODER_THREADS=N host rANS threads per rank (default: the "
+                                        "CPU quota / affinity divided by LOCAL_WORLD_SIZE); RDEIC_RANK_BOUND=1 the "
+                                        "launcher bound each rank to its own cores (the affinity set is not divided; "
+                                        "detected when it is at most 1 / LOCAL_WORLD_SIZE of the machine)")
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (one rank each); default: WORLD_SIZE under torch.distributed.run, else 1")
     ap.add_argument("--steps", type=int, default=5)

@@ -116,7 +116,10 @@ def default_threads() -> int:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
-    n = aff if os.environ.get("RDEIC_RANK_BOUND") == "1" else aff // lws
+    # ranks bound to their own cores: declared (RDEIC_RANK_BOUND=1), or an affinity set no larger than this rank's
+    # share of the machine (a launcher's per-rank binding, e.g. 6 cores of 48 with 8 ranks)
+    bound = os.environ.get("RDEIC_RANK_BOUND") == "1" or (lws > 1 and aff * lws <= (os.cpu_count() or aff))
+    n = aff if bound else aff // lws
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
             quota, period = f.read().split()[:2]

@@ -233,8 +233,9 @@ def test_default_threads_shared_among_local_ranks(monkeypatch):
 
 
 def test_default_threads_respects_per_rank_binding(monkeypatch):
-    """The affinity set is divided among the node's ranks unless the launcher declares per-rank binding
-    (RDEIC_RANK_BOUND=1): a cpuset-limited container (affinity < os.cpu_count(), no quota) is shared by
+    """The affinity set is divided among the node's ranks unless the ranks are bound to their own cores (declared
+    by RDEIC_RANK_BOUND=1, or detected: an affinity set of at most 1 / LOCAL_WORLD_SIZE of the machine): a
+    cpuset-limited container (affinity < os.cpu_count(), no quota) is shared by
     every rank, and RDEIC_CODER_THREADS overrides everything."""
     import os
     monkeypatch.delenv("RDEIC_CODER_THREADS", raising=False)
@@ -252,8 +253,10 @@ def test_default_threads_respects_per_rank_binding(monkeypatch):
     monkeypatch.setattr(builtins, "open", no_quota)
     assert coders.default_threads() == 8          # cpuset of 64 shared by 8 ranks, not 8 x 16
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(6)), raising=False)
-    assert coders.default_threads() == 1          # 6 // 8, at least one
+    assert coders.default_threads() == 6          # 6 x 8 ranks <= 256: a per-rank binding, detected
+    monkeypatch.setattr(os, "cpu_count", lambda: 40)
+    assert coders.default_threads() == 1          # 6 x 8 > 40: a shared cpuset, 6 // 8, at least one
     monkeypatch.setenv("RDEIC_RANK_BOUND", "1")
-    assert coders.default_threads() == 6          # bound per rank: 6 own cores
+    assert coders.default_threads() == 6          # declared per-rank binding: 6 own cores
     monkeypatch.setenv("RDEIC_CODER_THREADS", "3")
     assert coders.default_threads() == 3

@@ -29,7 +29,7 @@ TOL = 2e-3
 # float64 truth (TOL64), where ours measure 5.7e-5 (128^2) and 1.71e-3 (512^2) at worst (r05,
 # tools/grad_dump.py): >= 3x margin, and our worst may not exceed the reference fp32's own worst by > 1.5x
 # (512^2: 1.71e-3 against 1.81e-3).
-TOL_BY_SIZE = {128: 2e-3, 512: 7.5e-3}  # vs the fp32 golden: two independent fp32 results (worst 2.36e-3)
+TOL_BY_SIZE = {128: 2e-3, 512: 5e-3}    # vs the fp32 golden: two independent fp32 results (worst 2.36e-3, ~2.1x)
 TOL64 = {128: 2e-4, 512: 5.5e-3}        # vs the float64 truth (worst 5.7e-5 / 1.71e-3)
 REL_FLOOR = {128: 1e-4, 512: 0.0}       # ours-vs-reference accuracy bar floor (both ~1e-5 at 128^2)
 
