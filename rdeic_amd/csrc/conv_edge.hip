@@ -64,20 +64,20 @@ __global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int ntiles)
   for (int j = 0; j < 2; ++j) bias[j] = a.bias ? a.bias[c0 + 16 * j + lr] : 0.f;
   bf16x8 af[3][4];
   auto load_a = [&](int m0) {  // A fragments of the 64 pixels from m0 (one 16-byte pixel load per tap)
+    // the tile is 64 pixels of one image row (w % 64 == 0): its (image, row, column) once, on the scalar unit
+    const int img = __builtin_amdgcn_readfirstlane(m0 / hw), rem = __builtin_amdgcn_readfirstlane(m0 - img * hw);
+    const int y0 = __builtin_amdgcn_readfirstlane(rem / a.w), x0 = __builtin_amdgcn_readfirstlane(rem - y0 * a.w);
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       const int tap = 4 * s + lq;
       const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+      const int iy = y0 + ky - 1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = m0 + i * 16 + lr;
+        const int ix = x0 + i * 16 + lr + kx - 1;
         bf16x8 v = {};
-        if (tap < 9 && m < a.M) {
-          const int img = m / hw, rem = m - img * hw;
-          const int iy = rem / a.w + ky - 1, ix = rem - (rem / a.w) * a.w + kx - 1;
-          if ((unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w)
-            v = *reinterpret_cast<const bf16x8*>(in + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
-        }
+        if (tap < 9 && m0 < a.M && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w)
+          v = *reinterpret_cast<const bf16x8*>(in + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
         af[s][i] = v;
       }
     }
@@ -166,7 +166,6 @@ __global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int ntiles)
 // k order: 32-channel block major, tap minor (as the halo convs); fp32 accumulation.
 // ============================================================================================
 constexpr int NR_TC = 64, NR_HC = NR_TC + 2;
-constexpr int NR_AB_MAX = 512;  // input channels whose (a, b) table fits the LDS
 template <int TR> struct Narrow {
   static constexpr int NT = TR * 64, HPIX = (TR + 2) * NR_HC, ITEMS = HPIX * 4;  // 16-byte chunks per halo
   static constexpr int IPT = (ITEMS + NT - 1) / NT;
@@ -196,6 +195,14 @@ __global__ __launch_bounds__(TR * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
 
   for (int i = tid; i < cin / 2; i += NR::NT)
     reinterpret_cast<float4*>(abl)[i] = reinterpret_cast<const float4*>(a.gn_ab + (long)img * cin * 2)[i];
+  // the packed weights of the cout rows in LDS after the table: the MFMA phase then issues no global load, which
+  // would wait (in-order vmcnt) behind the next blocks' raw chunks in flight
+  char* const wl = lds + NR::LDS + cin * 8;
+  const int wrow = 9 * cin;
+  for (int i = tid; i < a.cout * wrow / 8; i += NR::NT) {
+    const int r = i / (wrow / 8), c = i - r * (wrow / 8);
+    reinterpret_cast<uint4*>(wl)[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.weight) + (long)r * a.wld + c * 8);
+  }
   // per item: the chunk's element offset in the input (-1: outside the image / past the halo) and its LDS slot,
   // the same for every channel block (computed once)
   int goff[NR::IPT], loff[NR::IPT];
@@ -251,10 +258,10 @@ __global__ __launch_bounds__(TR * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     for (int t = 0; t < 9; ++t) {
       const int ky = t / 3, kx = t - (t / 3) * 3;
       // per-tap addresses from laundered bases (hoisted, the 36 fragment addresses would spill)
-      int lb = wave * NR_HC + lr, wb = lr * a.wld + cb + 8 * lq;
+      int lb = wave * NR_HC + lr, wb = lr * wrow + cb + 8 * lq;
       asm volatile("" : "+v"(lb), "+v"(wb));
       bf16x8 bfv = {};
-      if (lr < a.cout) bfv = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.weight) + wb + t * cin);
+      if (lr < a.cout) bfv = *reinterpret_cast<const bf16x8*>(wl + (wb + t * cin) * 2);
       const int hp0 = lb + ky * NR_HC + kx;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // + 16 i keeps the swizzle (bits 2 of the pixel index unchanged)
@@ -297,7 +304,7 @@ int launch_edge(const rdeic_conv_desc* d, const ConvArgs& a, hipStream_t s, bool
       ((uintptr_t)d->in0) % 16 || ((uintptr_t)d->weight) % 16)
     return -1;
   // conv_in: 8 input channels, bias only, bf16 output, statistics per image (64-row blocks)
-  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout % 32 == 0 && d->cout <= 128 && !d->emb && !d->act && !d->res &&
+  if (d->c0 == 8 && !d->gn_ab && d->wld >= 128 && d->cout % 32 == 0 && d->cout <= 128 && d->w % 64 == 0 && !d->emb && !d->act && !d->res &&
       !d->out_f32 && !d->ln_rows && d->out_ld % 8 == 0 && ((uintptr_t)d->out) % 16 == 0) {
     ConvArgs e = a;
     const bool stats = e.gn_part != nullptr && e.gn_hw > 0 && e.gn_hw % 64 == 0;
@@ -316,14 +323,15 @@ int launch_edge(const rdeic_conv_desc* d, const ConvArgs& a, hipStream_t s, bool
     hipLaunchKernelGGL(conv_in8_kernel, dim3((unsigned)blocks), dim3(CI_NT), 4 * CI_WLDS, s, e, ntiles);
     return launch_status();
   }
-  // norm -> (SiLU) -> conv to <= 16 channels
+  // norm -> (SiLU) -> conv to <= 16 channels (table + weights in LDS beside the halo)
   constexpr int TR = 16;
-  if (d->gn_ab && d->cout <= 16 && d->c0 % 32 == 0 && d->c0 <= NR_AB_MAX && d->h % TR == 0 && d->w % NR_TC == 0 &&
-      !d->gn_part && !d->emb && ((uintptr_t)d->gn_ab) % 16 == 0) {
+  if (d->gn_ab && d->cout <= 16 && d->c0 % 32 == 0 && d->h % TR == 0 && d->w % NR_TC == 0 &&
+      Narrow<TR>::LDS + d->c0 * 8 + d->cout * 9 * d->c0 * 2 <= 160 * 1024 && !d->gn_part && !d->emb &&
+      ((uintptr_t)d->gn_ab) % 16 == 0) {
     rdeic_count_launch(RDEIC_COUNT_EDGE);
     const int tx = d->w / NR_TC, ty = d->h / TR;
     const dim3 g((unsigned)((long)d->n * ty * tx));
-    const int lds = Narrow<TR>::LDS + d->c0 * 8;
+    const int lds = Narrow<TR>::LDS + d->c0 * 8 + d->cout * 9 * d->c0 * 2;
     if (d->gn_silu) hipLaunchKernelGGL((conv3x3_gn_narrow_kernel<TR, true>), g, dim3(TR * 64), lds, s, a, tx, ty);
     else hipLaunchKernelGGL((conv3x3_gn_narrow_kernel<TR, false>), g, dim3(TR * 64), lds, s, a, tx, ty);
     return launch_status();

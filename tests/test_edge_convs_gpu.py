@@ -42,7 +42,7 @@ def _conv_in_run(x8, p, stats, edge):
         ops.set_edge_conv(prev)
 
 
-@pytest.mark.parametrize("n,h,w,stats", [(2, 64, 128, True), (1, 40, 37, False), (3, 16, 64, True), (1, 512, 512, True)])
+@pytest.mark.parametrize("n,h,w,stats", [(2, 64, 128, True), (1, 40, 64, False), (3, 16, 64, True), (1, 512, 512, True)])
 def test_conv_in8_bit_identical_and_vs_torch(gpu, n, h, w, stats):
     from rdeic_amd import ops
     g = torch.Generator().manual_seed(n * h + w)
