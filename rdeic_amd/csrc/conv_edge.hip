@@ -36,7 +36,7 @@ constexpr int CI_WLDS = 64 * CI_ROWB; // per wave
 // Persistent: block b takes the 64-pixel tiles b, b + grid, ... (all cout <= 128 channels each); every wave
 // issues the next tile's A loads right after its MFMAs consumed the current ones, so they fly under the epilogue.
 // ~150 VGPRs: three 4-wave blocks per CU.
-__global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int ntiles) {
+__global__ __launch_bounds__(CI_NT) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_in8_kernel(ConvArgs a, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -62,9 +62,13 @@ __global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int ntiles)
   float bias[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias[j] = a.bias ? a.bias[c0 + 16 * j + lr] : 0.f;
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rsi = __builtin_amdgcn_make_buffer_rsrc((void*)a.in0, (short)0,
+                                                                      (int)((long)a.M * a.ld0 * 2), 0x00020000);
   bf16x8 af[3][4];
   auto load_a = [&](int m0) {  // A fragments of the 64 pixels from m0 (one 16-byte pixel load per tap)
-    // the tile is 64 pixels of one image row (w % 64 == 0): its (image, row, column) once, on the scalar unit
+    // the tile is 64 pixels of one image row (w % 64 == 0): its (image, row, column) once, on the scalar unit;
+    // padding / the zero tail of k read zeros through the buffer descriptor (voffset kOOB), no branches
     const int img = __builtin_amdgcn_readfirstlane(m0 / hw), rem = __builtin_amdgcn_readfirstlane(m0 - img * hw);
     const int y0 = __builtin_amdgcn_readfirstlane(rem / a.w), x0 = __builtin_amdgcn_readfirstlane(rem - y0 * a.w);
 #pragma unroll
@@ -75,10 +79,10 @@ __global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int ntiles)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ix = x0 + i * 16 + lr + kx - 1;
-        bf16x8 v = {};
-        if (tap < 9 && m0 < a.M && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w)
-          v = *reinterpret_cast<const bf16x8*>(in + ((long)(img * a.h + iy) * a.w + ix) * a.ld0);
-        af[s][i] = v;
+        const bool ok = tap < 9 && m0 < a.M && (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+        const unsigned vo = ok ? (unsigned)(((img * a.h + iy) * a.w + ix) * a.ld0) * 2u : kOOB;
+        const u4v r = __builtin_amdgcn_raw_buffer_load_b128(rsi, vo, 0, 0);
+        af[s][i] = __builtin_bit_cast(bf16x8, r);
       }
     }
   };
@@ -155,14 +159,14 @@ __global__ __launch_bounds__(CI_NT) void conv_in8_kernel(ConvArgs a, int ntiles)
 // ============================================================================================
 // norm -> SiLU -> 3x3 conv to a few channels (cout <= 16; the decoder's conv_out 128 -> 3, fp32 output).
 // A block owns TR x 64 output pixels (TR waves, one output row each). Per 32-channel block of the input, the
-// threads load the (TR + 2) x 66 halo of the RAW input (16 bytes each: coalesced 64-byte pixel slices), apply the
-// GroupNorm affine + SiLU ONCE per element in registers (rdeic_groupnorm_apply's formula: fma, then
-// x * rcp(1 + e^-x), rounded to bf16; the affine / add / multiply two elements per packed-f32 instruction, which
-// is bit-identical to the scalar form) and write it to LDS; then every wave runs the 9 taps as 16x16x32 MFMAs with
-// N = 16 (cout real columns, the rest zero weights) reading its A fragments from the halo. The next block's raw
-// loads are issued before this block's MFMAs (register double buffering), and two blocks share a CU, so the HBM
-// stream runs under the transform. The transform is (TR + 2) / TR x 66 / 64 of the element count; it is the VALU
-// floor (two transcendentals per element), the MFMA work ~15% of it.
+// threads load the (TR + 2) x 66 halo of the RAW input (buffer loads, 16 bytes each: coalesced 64-byte pixel
+// slices; zeros outside the image from the descriptor's range check), apply the GroupNorm affine + SiLU ONCE per
+// element in registers (fma, then x * rcp(1 + e^-x) with e^-x as one v_exp_f32, rounded to bf16; scalar f32: packed
+// pairs cost a register move per operand around the scalar exp / rcp) and write it to LDS; then every wave runs the
+// 9 taps as 16x16x32 MFMAs with N = 16 (cout real columns, the rest zero weights) reading its A fragments from the
+// halo and its B fragments from the weights staged in LDS (a global load there would wait, in-order vmcnt, behind
+// the prefetched halo chunks). The raw chunks of the next two channel blocks are in flight (each reloaded right
+// after its transform). The transform is (TR + 2) / TR x 66 / 64 of the element count.
 // k order: 32-channel block major, tap minor (as the halo convs); fp32 accumulation.
 // ============================================================================================
 constexpr int NR_TC = 64, NR_HC = NR_TC + 2;
@@ -203,53 +207,57 @@ __global__ __launch_bounds__(TR * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
     const int r = i / (wrow / 8), c = i - r * (wrow / 8);
     reinterpret_cast<uint4*>(wl)[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.weight) + (long)r * a.wld + c * 8);
   }
-  // per item: the chunk's element offset in the input (-1: outside the image / past the halo) and its LDS slot,
-  // the same for every channel block (computed once)
-  int goff[NR::IPT], loff[NR::IPT];
+  // per item: the chunk's byte offset in the input (kOOB: outside the image / past the halo: the buffer
+  // descriptor's range check reads zeros, no branch) and its LDS slot, the same for every channel block
+  const __amdgpu_buffer_rsrc_t rsi = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.in0, (short)0, (int)((long)a.n * H * W * a.ld0 * 2), 0x00020000);
+  unsigned goff[NR::IPT];
+  int loff[NR::IPT];
 #pragma unroll
   for (int k = 0; k < NR::IPT; ++k) {
     const int it = tid + k * NR::NT, hp = it >> 2;
     const int hr = hp / NR_HC, hc = hp - (hp / NR_HC) * NR_HC;
     const int iy = oy0 - 1 + hr, ix = ox0 - 1 + hc;
     goff[k] = (it < NR::ITEMS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-                  ? ((img * H + iy) * W + ix) * a.ld0 + 8 * q : -1;
+                  ? (unsigned)(((img * H + iy) * W + ix) * a.ld0 + 8 * q) * 2u : kOOB;
     loff[k] = it < NR::ITEMS ? hp * 64 + ((q ^ nr_sw(hp)) << 4) : -1;
   }
   // raw chunks of two channel blocks in flight (the HBM latency is ~2 blocks of transform + MFMA)
-  uint4 raw0[NR::IPT], raw1[NR::IPT];
-  auto load = [&](uint4 (&raw)[NR::IPT], int cb, int k) {
-    raw[k] = uint4{0u, 0u, 0u, 0u};
-    if (goff[k] >= 0 && cb < cin) raw[k] = *reinterpret_cast<const uint4*>(in + goff[k] + cb);
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  u4v raw0[NR::IPT], raw1[NR::IPT];
+  auto load = [&](u4v (&raw)[NR::IPT], int cb, int k) {
+    if (cb < cin) raw[k] = __builtin_amdgcn_raw_buffer_load_b128(rsi, goff[k], cb * 2, 0);
   };
   f32x4 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   // one channel block: transform its raw chunks into the halo (reloading the registers with block cb + 64), then
   // the 9 taps
-  auto step = [&](uint4 (&raw)[NR::IPT], int cb) {
+  auto step = [&](u4v (&raw)[NR::IPT], int cb) {
     bar();  // the (a, b) table is in LDS / the previous block's MFMA reads of the halo are done
+    const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb + 8 * q) * 2);
+    const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
+    const float av[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
+    const float bv[8] = {t0.y, t0.w, t1.y, t1.w, t2.y, t2.w, t3.y, t3.w};
 #pragma unroll
     for (int k = 0; k < NR::IPT; ++k) {
-      uint4 o = uint4{0u, 0u, 0u, 0u};
-      if (goff[k] >= 0) {  // outside: the normalised tensor's zero pad
-        const float4* ab4 = reinterpret_cast<const float4*>(abl + (cb + 8 * q) * 2);
-        const float4 t0 = ab4[0], t1 = ab4[1], t2 = ab4[2], t3 = ab4[3];
-        const f32x2 av[4] = {{t0.x, t0.z}, {t1.x, t1.z}, {t2.x, t2.z}, {t3.x, t3.z}};
-        const f32x2 bv[4] = {{t0.y, t0.w}, {t1.y, t1.w}, {t2.y, t2.w}, {t3.y, t3.w}};
-        const unsigned w4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
-        unsigned o4[4];
+      // scalar f32 (packed pairs cost a register move per operand around the scalar exp / rcp); computed for every
+      // chunk and zeroed outside the image (the normalised tensor's zero pad) with a select, not a branch
+      const unsigned w4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+      unsigned o4[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {  // channels 2e, 2e + 1 of the chunk
-          f32x2 x = pk_fma(f32x2{__uint_as_float(w4[e] << 16), __uint_as_float(w4[e] & 0xffff0000u)}, av[e], bv[e]);
-          if constexpr (SILU) {
-            const f32x2 d = f32x2{__expf(-x.x), __expf(-x.y)} + 1.0f;
-            x *= f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-          }
-          const bf16 lo = (bf16)x.x, hi = (bf16)x.y;
-          o4[e] = (unsigned)__builtin_bit_cast(unsigned short, lo) | ((unsigned)__builtin_bit_cast(unsigned short, hi) << 16);
+      for (int e = 0; e < 4; ++e) {  // channels 2e, 2e + 1 of the chunk
+        float x0 = __builtin_fmaf(__uint_as_float(w4[e] << 16), av[2 * e], bv[2 * e]);
+        float x1 = __builtin_fmaf(__uint_as_float(w4[e] & 0xffff0000u), av[2 * e + 1], bv[2 * e + 1]);
+        if constexpr (SILU) {  // e^-x as one v_exp of -x log2(e) (the last layer's fp32 output, no bit-parity partner)
+          x0 *= __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x0 * -1.4426950408889634f));
+          x1 *= __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x1 * -1.4426950408889634f));
         }
-        o = uint4{o4[0], o4[1], o4[2], o4[3]};
+        typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+        o4[e] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{x0, x1}, bf16x2_t));  // one v_cvt_pk_bf16_f32
       }
+      const bool in_img = goff[k] != kOOB;
+      const uint4 o = in_img ? uint4{o4[0], o4[1], o4[2], o4[3]} : uint4{0u, 0u, 0u, 0u};
       if (loff[k] >= 0) *reinterpret_cast<uint4*>(lds + loff[k]) = o;
       load(raw, cb + 64, k);  // two blocks ahead
     }
