@@ -90,6 +90,7 @@ __global__ __launch_bounds__(CI_NT) __attribute__((amdgpu_waves_per_eu(3, 3))) v
   if (t < ntiles) load_a(t * 64);
   for (; t < ntiles; t += gridDim.x) {
     const int m0 = t * 64;  // this wave's 64 pixels
+    const bool full = m0 + 64 <= a.M;  // wave-uniform: no per-row checks
     f32x4 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -123,23 +124,29 @@ __global__ __launch_bounds__(CI_NT) __attribute__((amdgpu_waves_per_eu(3, 3))) v
       const int row = 16 * k + (lane >> 2), ch = lane & 3;
       const unsigned* src = reinterpret_cast<const unsigned*>(W + row * CI_ROWB + ch * 16);
       const uint4 v = uint4{src[0], src[1], src[2], src[3]};
-      if (m0 + row < a.M) *reinterpret_cast<uint4*>(out + (long)(m0 + row) * a.out_ld + c0 + ch * 8) = v;
+      if (full || m0 + row < a.M) *reinterpret_cast<uint4*>(out + (long)(m0 + row) * a.out_ld + c0 + ch * 8) = v;
     }
     if (a.gn_part) {
       const int p2 = lane & 15, g = lane >> 4;  // channels c0 + 2 p2, + 1; rows 16 g .. 16 g + 15
-      const int nv = a.M - (m0 + 16 * g);       // valid rows of the group
+      const int nv = full ? 16 : a.M - (m0 + 16 * g);  // valid rows of the group (wave-uniform test: full tile)
       float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+      unsigned w[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const unsigned w = *reinterpret_cast<const unsigned*>(W + (16 * g + r) * CI_ROWB + p2 * 4);
-        if (r < nv) {
-          const float y[2] = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+      for (int r = 0; r < 16; ++r) w[r] = *reinterpret_cast<const unsigned*>(W + (16 * g + r) * CI_ROWB + p2 * 4);
+      auto acc_row = [&](int r) {
+        const float y[2] = {__uint_as_float(w[r] << 16), __uint_as_float(w[r] & 0xffff0000u)};
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            s1[e] += y[e];
-            s2[e] = fmaf(y[e], y[e], s2[e]);
-          }
+        for (int e = 0; e < 2; ++e) {
+          s1[e] += y[e];
+          s2[e] = fmaf(y[e], y[e], s2[e]);
         }
+      };
+      if (full) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc_row(r);
+      } else {
+        for (int r = 0; r < 16; ++r)
+          if (r < nv) acc_row(r);
       }
       float t1[2], t2[2];
 #pragma unroll
