@@ -613,8 +613,8 @@ def _edge_narrow_eligible(x, x2, p: "ConvParams", up2, pad_t, pad_l, out_hw, spe
     n, h, w, c = x.shape
     if out_hw is not None and tuple(out_hw) != (h, w):
         return False
-    lds = 18 * 66 * 64 + c * 8 + p.cout * 9 * c * 2  # halo, GroupNorm table, weights (conv_edge.hip)
-    return p.cout <= 16 and c % 32 == 0 and lds <= 160 * 1024 and h % 16 == 0 and w % 64 == 0 \
+    lds = 10 * 66 * 64 + c * 8 + p.cout * 9 * c * 2  # 8-row halo, GroupNorm table, weights (conv_edge.hip)
+    return p.cout <= 16 and c % 32 == 0 and lds <= 160 * 1024 and h % 8 == 0 and w % 64 == 0 \
         and x.stride(2) % 8 == 0 and x.data_ptr() % 16 == 0
 
 

@@ -42,17 +42,18 @@ def _conv_in_run(x8, p, stats, edge):
         ops.set_edge_conv(prev)
 
 
-@pytest.mark.parametrize("n,h,w,stats", [(2, 64, 128, True), (1, 40, 64, False), (3, 16, 64, True), (1, 512, 512, True)])
-def test_conv_in8_bit_identical_and_vs_torch(gpu, n, h, w, stats):
+@pytest.mark.parametrize("n,h,w,stats,cout", [(2, 64, 128, True, 128), (1, 40, 64, False, 128), (3, 16, 64, True, 64),
+                                               (1, 512, 512, True, 128), (2, 8, 64, True, 96)])
+def test_conv_in8_bit_identical_and_vs_torch(gpu, n, h, w, stats, cout):
     from rdeic_amd import ops
     g = torch.Generator().manual_seed(n * h + w)
     x = torch.rand(n, 3, h, w, generator=g) * 2 - 1
-    wt = torch.randn(128, 3, 3, 3, generator=g) / math.sqrt(27)
-    b = torch.randn(128, generator=g) * 0.1
+    wt = torch.randn(cout, 3, 3, 3, generator=g) / math.sqrt(27)
+    b = torch.randn(cout, generator=g) * 0.1
     x8 = torch.zeros(n, h, w, 8)
     x8[..., :3] = x.permute(0, 2, 3, 1)
     x8 = x8.to(torch.bfloat16).cuda()
-    w8 = torch.zeros(128, 8, 3, 3)
+    w8 = torch.zeros(cout, 8, 3, 3)
     w8[:, :3] = wt
     p = ops.ConvParams.pack(w8, b, pad=1, dtype=torch.bfloat16)
     y1, ab1, ran1 = _conv_in_run(x8, p, stats, 1)
@@ -74,7 +75,7 @@ def _narrow_ref(x, gamma, beta, wt, b, silu):
 
 
 @pytest.mark.parametrize("n,cin,cout,h,w,silu", [(2, 128, 3, 32, 64, True), (1, 256, 4, 16, 128, True),
-                                                 (3, 64, 16, 48, 64, False), (1, 128, 3, 512, 512, True)])
+                                                 (3, 64, 16, 40, 64, False), (1, 128, 3, 512, 512, True)])
 def test_narrow_gn_conv_vs_torch_and_materialised(gpu, n, cin, cout, h, w, silu):
     from rdeic_amd import ops
     g = torch.Generator().manual_seed(cin * cout + h)

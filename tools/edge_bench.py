@@ -1,7 +1,8 @@
 """Times the VAE edge convs (conv_edge.hip) and the fused GroupNorm finalize + apply on the bench's shapes,
 each against the path it replaced (same process, alternating, HIP events on the launch stream).
 
-  python tools/edge_bench.py [REPS]   (GPU box) -> one JSON line per case
+  python tools/edge_bench.py [REPS] [only]   (GPU box) -> one JSON line per case
+  only: the edge kernels alone, no replaced paths, no GroupNorm cases (PMC runs)
 """
 import json
 import math
@@ -28,6 +29,7 @@ def timed(fn, reps):
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    only = len(sys.argv) > 2 and sys.argv[2] == "only"
     torch.manual_seed(0)
     n, h, w = 16, 512, 512
     # conv_in: 8 (3 real) -> 128, with the GroupNorm statistics of the output
@@ -49,8 +51,15 @@ def main():
     }
     for name, (fn, byts) in cases.items():
         res = {}
+        modes = (1, 0)
+        if only:
+            prev = ops.set_edge_conv(1)
+            ms = timed(fn, reps)
+            ops.set_edge_conv(prev)
+            print(json.dumps({"case": name, "ms": round(ms, 4)}), flush=True)
+            continue
         for _ in range(2):
-            for edge in (1, 0):
+            for edge in modes:
                 prev = ops.set_edge_conv(edge)
                 try:
                     ms = timed(fn, reps)
@@ -58,9 +67,12 @@ def main():
                     ops.set_edge_conv(prev)
                 res.setdefault(edge, []).append(ms)
         e, o = min(res[1]), min(res[0])
-        print(json.dumps({"case": name, "edge_ms": round(e, 4), "edge_TBps": round(byts / e / 1e9, 2),
+        extra = {f"mode{m}_ms": round(min(v), 4) for m, v in res.items() if m > 1}
+        print(json.dumps({"case": name, **extra, "edge_ms": round(e, 4), "edge_TBps": round(byts / e / 1e9, 2),
                           "replaced_ms": round(o, 4), "replaced_TBps": round(byts / o / 1e9, 2),
                           "algorithmic_bytes": byts}), flush=True)
+    if only:
+        return
     # fused GroupNorm finalize + apply vs parts_ab + apply (the UNet's 16^2 / 8^2 GroupNorms)
     for (hh, c0, c1) in ((16, 1280, 0), (16, 1280, 1280), (8, 1280, 0), (8, 1280, 1280), (16, 640, 640)):
         xa = torch.randn(n, hh, hh, 256, device="cuda").to(torch.bfloat16)
