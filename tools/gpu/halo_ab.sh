@@ -25,8 +25,8 @@ import json, collections, sys
 agg = collections.defaultdict(list)
 for l in open(sys.argv[1]):
     d = json.loads(l); r = d['r']; c = r['cycles']
-    agg[(d['v'], r['shape'][1], r['shape'][3], r['shape'][4])].append((r['ms'], c['main_med'], c['block_med']))
+    agg[(d['v'], r['shape'][1], r['shape'][3], r['shape'][4])].append((r['ms'], c['main_med'], c['block_med'], c['epilogue_med'], c['prologue_med'], r.get('epi_overlap', 0)))
 for k, v in agg.items():
     med = lambda i: sorted(x[i] for x in v)[len(v) // 2]
-    print(k, 'ms', round(sum(x[0] for x in v) / len(v), 4), 'main', med(1), 'block', med(2))
+    print(k, 'ms', round(sum(x[0] for x in v) / len(v), 4), 'pro', med(4), 'main', med(1), 'epi', med(3), 'block', med(2), 'epi_overlap', med(5))
 PY

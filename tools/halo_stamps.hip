@@ -3,13 +3,18 @@
 // and runs the halo conv on one layer shape with random operands, through the library's own dispatch
 // (rdeic_conv2d). Prints the event-timed launch and the per-block phase split.
 //
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/halo_stamps.hip -o tools/halo_stamps \
-//         -Lrdeic_amd/lib -lrdeic_hip -Wl,-rpath,'$ORIGIN/../rdeic_amd/lib'
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -fno-slp-vectorize tools/halo_stamps.hip -o tools/halo_stamps_cur
+//   (self-contained: linking librdeic_hip.so let its registration of the same kernel names win, so the stamped
+//   kernels never ran)
 //   tools/halo_stamps N H W C COUT [res stats]
 #define RDEIC_HALO_STAMPS 1
 #include "../rdeic_amd/csrc/conv_gemm.hip"
 #include "../rdeic_amd/csrc/conv_dma.hip"
 #include "../rdeic_amd/csrc/conv_halo.hip"
+#include "../rdeic_amd/csrc/conv_edge.hip"
+#include "../rdeic_amd/csrc/prof.hip"
+#include "../rdeic_amd/csrc/norm.hip"
+#include "../rdeic_amd/csrc/attention.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -127,6 +132,29 @@ int main(int argc, char** argv) {
     conc += busy / (double)(z - a);
     span_sum += (double)(z - a);
   }
+  // epilogue overlap: for each block, the share of its XCD's CUs whose blocks are in their epilogue at its
+  // epilogue's midpoint (~1 when the CUs run in lockstep, ~epilogue/block when they are de-phased)
+  std::map<long, std::vector<std::pair<unsigned long long, unsigned long long>>> epi_by_xcd;
+  std::map<long, std::map<long, int>> cus_by_xcd;
+  for (long b = 0; b < tiles; ++b) {
+    const unsigned long long* q = &h[b * 8];
+    const long xcc = (long)q[6] & 0xF, hw = (long)q[5];
+    epi_by_xcd[xcc].push_back({q[2], q[3]});
+    cus_by_xcd[xcc][((hw >> 8) & 0xF) * 256 + ((hw >> 13) & 0x7) * 16 + ((hw >> 16) & 0x3)] = 1;
+  }
+  double ov_sum = 0;
+  long ov_n = 0;
+  for (auto& kv : epi_by_xcd) {
+    auto& v = kv.second;
+    const double ncu = (double)cus_by_xcd[kv.first].size();
+    for (size_t i = 0; i < v.size(); i += 7) {  // sampled
+      const unsigned long long mid = v[i].first / 2 + v[i].second / 2;
+      int c = 0;
+      for (auto& e : v) c += (e.first <= mid && mid < e.second);
+      ov_sum += c / ncu;
+      ++ov_n;
+    }
+  }
   const double cyc_span = (double)(t1 - t0);
   const double clk_ghz = cyc_span / (ms * 1e6);
   // MFMA-bound floor per block: (9 taps x cin/32) x 16 MFMA x 16 cycles x waves per SIMD (2 or 4)
@@ -134,9 +162,9 @@ int main(int argc, char** argv) {
   printf("{\"shape\": [%d, %d, %d, %d, %d], \"res\": %d, \"stats\": %d, \"ms\": %.4f, \"tflops\": %.1f, "
          "\"blocks\": %ld, \"cus_seen\": %zu, \"clock_ghz_est\": %.3f, \"blocks_in_flight_per_cu\": %.2f, "
          "\"cycles\": {\"prologue_med\": %.0f, \"main_med\": %.0f, \"main_p90\": %.0f, \"epilogue_med\": %.0f, "
-         "\"epilogue_p90\": %.0f, \"block_med\": %.0f}, \"main_floor_cycles\": %.0f, \"tile_rows\": %d}\n",
+         "\"epilogue_p90\": %.0f, \"block_med\": %.0f}, \"main_floor_cycles\": %.0f, \"tile_rows\": %d, \"epi_overlap\": %.3f}\n",
          N, H, W, C, CO, use_res, use_stats, ms, flops / (ms * 1e-3) / 1e12, tiles, per_cu.size(), clk_ghz,
          conc / per_cu.size(), pct(pro, .5), pct(mainl, .5), pct(mainl, .9), pct(epi, .5), pct(epi, .9), pct(tot, .5),
-         floor_main, trow);
+         floor_main, trow, ov_n ? ov_sum / ov_n : 0.0);
   return 0;
 }
