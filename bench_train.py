@@ -38,6 +38,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--ft-splitk", default="short", choices=["short", "long", "off"],
+                    help="split-K policy of the step's convs (A/B; finetune.FT_SPLITK)")
     ap.add_argument("--eager", action="store_true",
                     help="eager steps (default on one GPU: the step captured once as a hipGraph and replayed)")
     return ap.parse_args(argv)
@@ -48,7 +50,9 @@ def main(argv=None):
     from rdeic_amd.launch import maybe_launch
     maybe_launch(args.gpus, __file__, sys.argv[1:] if argv is None else list(argv))
     from rdeic_amd import ops, parallel
+    from rdeic_amd import finetune
     from rdeic_amd.finetune import CapturedStep, FineTuner, nchw_draws_to_nhwc
+    finetune.FT_SPLITK = args.ft_splitk
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import synth_context, synth_image, train_draws
 

@@ -364,6 +364,96 @@ constexpr bool stats_tile_ok() {
   return (WTM == 32 || WTM == 64) && (WTM / P) % 16 == 0;
 }
 
+// Fused GEGLU epilogue (out_mode 2, attention.py:49-56): the packed weight interleaves 4 value rows with their 4
+// gate rows, so two adjacent 8-column chunks (x0..x3, g0..g3, x4..x7, g4..g7) are 8 consecutive outputs. Each
+// thread takes such chunk PAIRS and writes one 16-byte store per pair, where epilogue_vec writes one 8-byte store
+// per chunk: half the store instructions for the same bytes (a tile's epilogue is bound by the CU's
+// store-instruction rate, MI355X_MICROARCH.md). Per element the arithmetic is epilogue_vec's (LayerNorm fold,
+// bias, bf16 rounding of both halves, x * gelu(g)), so outputs are bit-identical to it. Needs cout % 16 == 0.
+template <int BM, int BN, int WGM, int WGN, int NT, int P>
+__device__ __forceinline__ void epilogue_geglu(const f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16], const ConvArgs& a,
+                                               int m0, int n0, int wm, int wn, int lane, int tid, char* lds) {
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int HM = TM / P;        // fragment rows per pass
+  constexpr int PR = BM / P;        // tile rows per pass
+  constexpr int SDW = BN + 4;       // LDS row stride in dwords
+  constexpr int DPR = BN / 16;      // chunk pairs per row
+  constexpr int ND = (PR * DPR + NT - 1) / NT;
+  static_assert(TM % P == 0 && BN % 16 == 0, "P passes, chunk pairs");
+  const int lr = lane & 15, lq = lane >> 4;
+  float* L = reinterpret_cast<float*>(lds);
+  auto bar = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    bar();  // the previous pass's LDS readers are done
+#pragma unroll
+    for (int ii = 0; ii < HM; ++ii)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pr = wm * (WTM / P) + ii * 16 + lq * 4 + r;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) L[pr * SDW + wn * WTN + j * 16 + lr] = acc[p * HM + ii][j][r];
+      }
+    bar();
+#pragma unroll
+    for (int k = 0; k < ND; ++k) {
+      const int d = tid + k * NT;
+      if (d >= PR * DPR) continue;
+      const int pr = d / DPR, cq = d - pr * DPR;
+      const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
+      const int m = m0 + wmr * WTM + p * (WTM / P) + wr;
+      const int nn = n0 + cq * 16;
+      if (m >= a.M || nn >= a.cout) continue;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(L + pr * SDW + cq * 16 + 4 * q);
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      }
+      if (a.ln_rows) {  // v = rstd * (v - mean * colsum), two columns per packed fma / mul
+        const float2 ms = reinterpret_cast<const float2*>(a.ln_rows)[m];
+        const f32x2 nm = {-ms.x, -ms.x}, rs = {ms.y, ms.y};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 c = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4 * q);
+          const float cs[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2 r = rs * pk_fma(nm, f32x2{cs[e], cs[e + 1]}, f32x2{v[4 * q + e], v[4 * q + e + 1]});
+            v[4 * q + e] = r.x;
+            v[4 * q + e + 1] = r.y;
+          }
+        }
+      }
+      if (a.bias) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 b = *reinterpret_cast<const float4*>(a.bias + nn + 4 * q);
+          const f32x2 r0 = f32x2{v[4 * q], v[4 * q + 1]} + f32x2{b.x, b.y};
+          const f32x2 r1 = f32x2{v[4 * q + 2], v[4 * q + 3]} + f32x2{b.z, b.w};
+          v[4 * q] = r0.x; v[4 * q + 1] = r0.y; v[4 * q + 2] = r1.x; v[4 * q + 3] = r1.y;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = apply_act(v[e], a.act, a.act_param);
+      bf16 gv[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const f32x2 xv = {to_f32(from_f32<bf16>(v[8 * h + e])), to_f32(from_f32<bf16>(v[8 * h + e + 1]))};
+          const f32x2 gt = {to_f32(from_f32<bf16>(v[8 * h + 4 + e])), to_f32(from_f32<bf16>(v[8 * h + 5 + e]))};
+          const f32x2 r = xv * gelu_fast2(gt);
+          gv[4 * h + e] = from_f32<bf16>(r.x);
+          gv[4 * h + e + 1] = from_f32<bf16>(r.y);
+        }
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.out) + (long)m * a.out_ld + (nn >> 1)) =
+          *reinterpret_cast<uint4*>(gv);
+    }
+  }
+}
+
 constexpr unsigned kOOB = 0x80000000u;  // voffset that reads zeros (buffers are < 2 GiB)
 
 template <int N>

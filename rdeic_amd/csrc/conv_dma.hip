@@ -70,7 +70,9 @@ __device__ __forceinline__ void epilogue_scalar(const f32x4 (&acc)[TM][TN], cons
 }
 
 // 64-deep k-tiles: 128-byte LDS rows, two 16x16x32 MFMA k-steps per tile.
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+// GEG: the fused-GEGLU instantiation (out_mode 2, epilogue_geglu); the others compile epilogue_vec only, so the
+// GEGLU epilogue's registers never count against the plain tiles
+template <int BM, int BN, int WGM, int WGN, int S, int EP, bool GEG = false>
 __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1,
                                               unsigned bytesw) {
   constexpr int KB = 64;
@@ -239,7 +241,8 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
   HALO_STAMP(2);
   if constexpr (TM % EP == 0 && (BM / EP) * (BN + 4) * 4 <= S * STAGE) {
     if ((a.epi_vec || a.out_mode == 2) && epi_vec_ok(a)) {
-      epilogue_vec<BM, BN, WGM, WGN, NT, EP>(acc, a, m0, n0, wm, wn, lane, tid, lds);
+      if constexpr (GEG) epilogue_geglu<BM, BN, WGM, WGN, NT, EP>(acc, a, m0, n0, wm, wn, lane, tid, lds);
+      else epilogue_vec<BM, BN, WGM, WGN, NT, EP>(acc, a, m0, n0, wm, wn, lane, tid, lds);
       HALO_STAMP(3);
       return;
     }
@@ -252,16 +255,16 @@ __device__ __forceinline__ void conv_dma_body(ConvArgs a, int tiles_n, unsigned 
 // hardware admits floor(800 / (ceil(sgpr / 16) * 16 + 16)) waves per SIMD; MI355X_MICROARCH.md
 // "Residency"), so the 16-wave 128x128 tile (64 KB of LDS: two blocks fit) is built with its
 // SGPR budget capped; the others keep the compiler's allocation.
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+template <int BM, int BN, int WGM, int WGN, int S, int EP, bool GEG = false>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_dma_kernel(ConvArgs a, int tiles_n, unsigned bytes0,
                                                                   unsigned bytes1, unsigned bytesw) {
-  conv_dma_body<BM, BN, WGM, WGN, S, EP>(a, tiles_n, bytes0, bytes1, bytesw);
+  conv_dma_body<BM, BN, WGM, WGN, S, EP, GEG>(a, tiles_n, bytes0, bytes1, bytesw);
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, int EP>
+template <int BM, int BN, int WGM, int WGN, int S, int EP, bool GEG = false>
 __global__ __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_num_sgpr(80))) void conv_dma_kernel_2pc(
     ConvArgs a, int tiles_n, unsigned bytes0, unsigned bytes1, unsigned bytesw) {
-  conv_dma_body<BM, BN, WGM, WGN, S, EP>(a, tiles_n, bytes0, bytes1, bytesw);
+  conv_dma_body<BM, BN, WGM, WGN, S, EP, GEG>(a, tiles_n, bytes0, bytes1, bytesw);
 }
 
 // DMA-path eligibility: bf16, 16-byte-aligned 64-channel blocks, every buffer < 2 GiB.
@@ -306,12 +309,24 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
   const long tiles = (long)cdiv(a.M, BM) * tn;
   dim3 grid((unsigned)tiles, 1, a.splits > 1 ? a.splits : a.batch);
   constexpr int lds = S * (BM + BN) * 128;
-  if constexpr (WGM * WGN == 16 && lds <= 80 * 1024)
-    hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0,
-                       b1, bw);
-  else
-    hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0, b1,
-                       bw);
+  // fused GEGLU with 16-byte chunk-pair stores (epilogue_geglu) where the vector epilogue runs
+  const bool geg = a.out_mode == 2 && a.cout % 16 == 0 && a.out_ld % 8 == 0 && ((uintptr_t)a.out % 16) == 0 &&
+                   dma_vec_epilogue<BM, BN, WGM, WGN, S, EP>(a);
+  if constexpr (WGM * WGN == 16 && lds <= 80 * 1024) {
+    if (geg)
+      hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP, true>), grid, dim3(WGM * WGN * 64), lds, s, a,
+                         tn, b0, b1, bw);
+    else
+      hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0,
+                         b1, bw);
+  } else {
+    if (geg)
+      hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP, true>), grid, dim3(WGM * WGN * 64), lds, s, a, tn,
+                         b0, b1, bw);
+    else
+      hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0, b1,
+                         bw);
+  }
   return launch_status();
 }
 }  // namespace

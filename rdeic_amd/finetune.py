@@ -46,6 +46,19 @@ class FineTuneConfig:
         self.vq_beta, self.vq_decay, self.vq_temp = vq_beta, vq_decay, vq_temp
 
 
+# Split-K policy of the fine-tune step (A/B switch, bench_train.py --ft-splitk): "short" (default) splits every
+# small-M layer with >= 8 k-tiles (ops.splitk_allowed(short_k=True)), "long" only the inference rule's >= 32
+# k-tile layers, "off" none (one launch per conv: no partial-sum reduce launches).
+FT_SPLITK = "short"
+
+
+def _ft_splitk_ctx():
+    import contextlib
+    if FT_SPLITK == "off":
+        return contextlib.nullcontext()
+    return ops.splitk_allowed(short_k=FT_SPLITK == "short")
+
+
 class FineTuner:
     """Holds the flat trainable parameters / grads / AdamW state of an RDEIC model and runs steps."""
 
@@ -390,7 +403,7 @@ class FineTuner:
             self.buckets.begin()
         # training needs no batch invariance anywhere: small-M / large-K convs (B=1 UNet levels, input
         # gradients) may split K (deterministic, fixed-order reduction)
-        with ops.splitk_allowed(short_k=True), AG.STEP_PACKS.active():
+        with _ft_splitk_ctx(), AG.STEP_PACKS.active():
             loss, d = self.losses(x_start, h, ctx, draws["t"], draws["noise"], draws["slice_noise"])
             loss.backward()
         if self.buckets is not None:
@@ -455,7 +468,7 @@ class CapturedStep:
         ft.zero_grad()
         AG.STEP_PACKS.refresh()
         x_start, h = ft.get_first_stage(self.img, self.d["post_eps"])
-        with ops.splitk_allowed(short_k=True), AG.STEP_PACKS.active():
+        with _ft_splitk_ctx(), AG.STEP_PACKS.active():
             loss, d = ft.losses(x_start, h, self.ctx, self.d["t"], self.d["noise"], self.d["slice_noise"])
             loss.backward()
         d = {k: v.detach() for k, v in d.items()}
