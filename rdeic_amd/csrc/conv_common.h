@@ -380,12 +380,41 @@ __device__ __forceinline__ void epilogue_geglu(const f32x4 (&acc)[BM / WGM / 16]
   constexpr int SDW = BN + 4;       // LDS row stride in dwords
   constexpr int DPR = BN / 16;      // chunk pairs per row
   constexpr int ND = (PR * DPR + NT - 1) / NT;
+  constexpr int NPF = ND < 2 ? ND : 2;      // LayerNorm row statistics prefetched per pass (as epilogue_vec)
+  constexpr bool HOIST = (NT % DPR) == 0;  // every pair of a thread has the same 16 columns
   static_assert(TM % P == 0 && BN % 16 == 0, "P passes, chunk pairs");
   const int lr = lane & 15, lq = lane >> 4;
   float* L = reinterpret_cast<float*>(lds);
   auto bar = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto row_of = [&](int d, int p) {
+    const int pr = d / DPR;
+    const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
+    return m0 + wmr * WTM + p * (WTM / P) + wr;
+  };
+  // bias / LayerNorm column sums of this thread's 16 columns, once (loaded before the first park)
+  float4 bh[4], chh[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bh[q] = chh[q] = float4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (HOIST) {
+    const int nn = n0 + (tid % DPR) * 16;
+    if (nn < a.cout) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (a.bias) bh[q] = *reinterpret_cast<const float4*>(a.bias + nn + 4 * q);
+        if (a.ln_rows) chh[q] = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4 * q);
+      }
+    }
+  }
 #pragma unroll
   for (int p = 0; p < P; ++p) {
+    float2 lpf[NPF];
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int d = tid + k * NT;
+      const int m = row_of(d, p);
+      lpf[k] = float2{0.f, 0.f};
+      if (a.ln_rows && d < PR * DPR && m < a.M) lpf[k] = reinterpret_cast<const float2*>(a.ln_rows)[m];
+    }
     bar();  // the previous pass's LDS readers are done
 #pragma unroll
     for (int ii = 0; ii < HM; ++ii)
@@ -401,8 +430,7 @@ __device__ __forceinline__ void epilogue_geglu(const f32x4 (&acc)[BM / WGM / 16]
       const int d = tid + k * NT;
       if (d >= PR * DPR) continue;
       const int pr = d / DPR, cq = d - pr * DPR;
-      const int wmr = pr / (WTM / P), wr = pr - wmr * (WTM / P);
-      const int m = m0 + wmr * WTM + p * (WTM / P) + wr;
+      const int m = row_of(d, p);
       const int nn = n0 + cq * 16;
       if (m >= a.M || nn >= a.cout) continue;
       float v[16];
@@ -412,11 +440,11 @@ __device__ __forceinline__ void epilogue_geglu(const f32x4 (&acc)[BM / WGM / 16]
         v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
       }
       if (a.ln_rows) {  // v = rstd * (v - mean * colsum), two columns per packed fma / mul
-        const float2 ms = reinterpret_cast<const float2*>(a.ln_rows)[m];
+        const float2 ms = k < NPF ? lpf[k < NPF ? k : 0] : reinterpret_cast<const float2*>(a.ln_rows)[m];
         const f32x2 nm = {-ms.x, -ms.x}, rs = {ms.y, ms.y};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 c = *reinterpret_cast<const float4*>(a.ln_cs + nn + 4 * q);
+          const float4 c = HOIST ? chh[q] : *reinterpret_cast<const float4*>(a.ln_cs + nn + 4 * q);
           const float cs[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
@@ -429,7 +457,7 @@ __device__ __forceinline__ void epilogue_geglu(const f32x4 (&acc)[BM / WGM / 16]
       if (a.bias) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 b = *reinterpret_cast<const float4*>(a.bias + nn + 4 * q);
+          const float4 b = HOIST ? bh[q] : *reinterpret_cast<const float4*>(a.bias + nn + 4 * q);
           const f32x2 r0 = f32x2{v[4 * q], v[4 * q + 1]} + f32x2{b.x, b.y};
           const f32x2 r1 = f32x2{v[4 * q + 2], v[4 * q + 3]} + f32x2{b.z, b.w};
           v[4 * q] = r0.x; v[4 * q + 1] = r0.y; v[4 * q + 2] = r1.x; v[4 * q + 3] = r1.y;

@@ -313,12 +313,10 @@ int launch_dma(ConvArgs a, unsigned b0, unsigned b1, unsigned bw, hipStream_t s,
   const bool geg = a.out_mode == 2 && a.cout % 16 == 0 && a.out_ld % 8 == 0 && ((uintptr_t)a.out % 16) == 0 &&
                    dma_vec_epilogue<BM, BN, WGM, WGN, S, EP>(a);
   if constexpr (WGM * WGN == 16 && lds <= 80 * 1024) {
-    if (geg)
-      hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP, true>), grid, dim3(WGM * WGN * 64), lds, s, a,
-                         tn, b0, b1, bw);
-    else
-      hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0,
-                         b1, bw);
+    // (no GEGLU instantiation here: its 76 VGPRs would leave one block per CU where the plain kernel's 63 fit two,
+    // 217 -> 298 us on the 320-channel GEGLU, profiles/r06_geglu_lin_bench.txt)
+    hipLaunchKernelGGL((conv_dma_kernel_2pc<BM, BN, WGM, WGN, S, EP>), grid, dim3(WGM * WGN * 64), lds, s, a, tn, b0,
+                       b1, bw);
   } else {
     if (geg)
       hipLaunchKernelGGL((conv_dma_kernel<BM, BN, WGM, WGN, S, EP, true>), grid, dim3(WGM * WGN * 64), lds, s, a, tn,

@@ -25,10 +25,17 @@ SHAPES = [
     ("vae_down128@512", 16, 512, 512, 128, 0, 128, 3, 2, 0, 0),
     ("unet320@64", 16, 64, 64, 320, 0, 320, 3, 1, 0, None),
     ("unet640@32", 16, 32, 32, 640, 0, 640, 3, 1, 0, None),
+    ("unet1280to640@32", 16, 32, 32, 1280, 0, 640, 3, 1, 0, None),
+    ("unet1920to640@32", 16, 32, 32, 1920, 0, 640, 3, 1, 0, None),
+    ("unet960to640@32", 16, 32, 32, 960, 0, 640, 3, 1, 0, None),
+    ("unet320to640@32", 16, 32, 32, 320, 0, 640, 3, 1, 0, None),
+    ("unet640to1280@16", 16, 16, 16, 640, 0, 1280, 3, 1, 0, None),
     ("unet1280@16", 16, 16, 16, 1280, 0, 1280, 3, 1, 0, None),
     ("unet1280@8", 16, 8, 8, 1280, 0, 1280, 3, 1, 0, None),
     ("unet_cat640+320@64", 16, 64, 64, 640, 320, 320, 3, 1, 0, None),
     ("unet_cat1280+1280@8", 16, 8, 8, 1280, 1280, 1280, 3, 1, 0, None),
+    ("unet_cat1280+1280@16", 16, 16, 16, 1280, 1280, 1280, 3, 1, 0, None),
+    ("unet_cat1280+640@16", 16, 16, 16, 1280, 640, 1280, 3, 1, 0, None),
     ("unet640to320@64", 16, 64, 64, 640, 0, 320, 3, 1, 0, None),
     ("unet960to320@64", 16, 64, 64, 960, 0, 320, 3, 1, 0, None),
     ("lin1280x320", 1, 65536, 1, 1280, 0, 320, 1, 1, 0, None),

@@ -22,7 +22,8 @@ TILES = (-1, 21, 22, 24, 25, 26, 27, 30, 31, 32, 33, 34, 36, 37, 38)
 
 
 def main():
-    only = sys.argv[1:]
+    only = [a for a in sys.argv[1:] if a != "--ln"]
+    ln = "--ln" in sys.argv[1:]  # the model's form: LayerNorm folded into the projection (ParamStore.conv_ln)
     torch.manual_seed(0)
     for name, M, K, N, res, geglu in SHAPES:
         if only and not any(o in name for o in only):
@@ -33,17 +34,24 @@ def main():
         st = ParamStore(torch.bfloat16, "cuda")
         st.shapes["l.weight"], st.shapes["l.bias"] = (N, K), (N,)
         st.t["l.weight"], st.t["l.bias"] = w, b
-        p = st.conv_geglu("l") if geglu else st.conv("l")
+        lnr = None
+        if ln:
+            st.shapes["n.weight"], st.shapes["n.bias"] = (K,), (K,)
+            st.t["n.weight"], st.t["n.bias"] = 1 + 0.1 * torch.randn(K, device="cuda"), 0.1 * torch.randn(K, device="cuda")
+            p = st.conv_ln(["l"], "n", geglu=geglu)
+            lnr = ops.layer_norm_rowstats(x)
+        else:
+            p = st.conv_geglu("l") if geglu else st.conv("l")
         nout = N // 2 if geglu else N
         r = torch.randn(M, nout, device="cuda").to(torch.bfloat16) if res else None
         out = torch.empty(M, nout, device="cuda", dtype=torch.bfloat16)
         flops = 2.0 * M * K * N
         bytes_ = 2.0 * (M * K + N * K + M * nout * (2 if res else 1))
-        row = {"name": name}
+        row = {"name": name + ("+ln" if ln else "")}
         for t in TILES:
             ops.FORCE_TILE = t if t >= 0 else None
             try:
-                fn = lambda: ops.linear(x, p, res=r, out=out, geglu=geglu, images=16)  # noqa: E731
+                fn = lambda: ops.linear(x, p, res=r, out=out, geglu=geglu, images=16, ln_rows=lnr)  # noqa: E731
                 fn()
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
