@@ -468,3 +468,47 @@ def test_conv_splitk_repeatable_with_stats(gpu, cin, cout, hw, B, act, res, emb,
         assert torch.equal(outs[0][0], y)
         if ab is not None:
             assert torch.equal(outs[0][1], ab)
+
+
+@pytest.mark.parametrize("levels,sorted_table", [(64, True), (64, False), (300, True), (2, True)])
+def test_ckbd_indexes_scale_table(gpu, levels, sorted_table):
+    """rdeic_ckbd_indexes / rdeic_ckbd_encode build_indexes (compressai GaussianConditional: L-1 - #{k: max(s, b) <=
+    table[k]}): the LDS table's binary search on a non-decreasing table and the linear count on any other table
+    (and on tables past the LDS capacity) give the reference's integers exactly, ties at table values included."""
+    from rdeic_amd import ops
+    g = torch.Generator().manual_seed(levels * 3 + int(sorted_table))
+    n, hy, wy, c = 2, 6, 8, 5
+    tab = torch.exp(torch.linspace(math.log(0.11), math.log(256.0), levels - 1))
+    if not sorted_table:
+        tab = tab[torch.randperm(levels - 1, generator=g)]
+    # scales: random, exact table values (ties) and values below the bound
+    scale = torch.exp(torch.rand(n, hy, wy, c, generator=g) * 7 - 3)
+    flat = scale.view(-1)
+    flat[::7] = tab[torch.randint(0, levels - 1, (flat[::7].numel(),), generator=g)]
+    flat[::11] = 0.01
+    params = torch.cat([scale, torch.randn(n, hy, wy, c, generator=g)], dim=3).contiguous()
+    y = torch.randn(n, hy, wy, c, generator=g) * 3
+    bound = 0.11
+    wq = wy // 2
+    for phase in (0, 1):
+        idx = torch.full((n, c * hy * wq), -1, dtype=torch.int32, device="cuda")
+        sym = torch.zeros_like(idx)
+        yhat = torch.zeros(n, hy, wy, c, device="cuda")
+        tab_d = tab.float().cuda()
+        ops.call("rdeic_ckbd_indexes", params.cuda().data_ptr(), 2 * c, n, hy, wy, c, phase, tab_d.data_ptr(), levels,
+                 bound, idx.data_ptr(), c * hy * wq, 0, 0, ops.stream_ptr())
+        idx2 = torch.full_like(idx, -1)
+        yc, pc = y.cuda(), params.cuda()
+        ops.call("rdeic_ckbd_encode", yc.data_ptr(), c, pc.data_ptr(), 2 * c, n, hy, wy, c, phase, tab_d.data_ptr(),
+                 levels, bound, sym.data_ptr(), idx2.data_ptr(), c * hy * wq, 0, yhat.data_ptr(), c, None, 0, 0,
+                 ops.stream_ptr())
+        torch.cuda.synchronize()
+        # reference over the squeezed lattice [c][hy][wy/2]
+        r = torch.arange(hy).view(hy, 1)
+        j = torch.arange(wq).view(1, wq)
+        col = (2 * j + 1 - (r & 1)) if phase == 0 else (2 * j + (r & 1))
+        s = scale[:, r, col, :].permute(0, 3, 1, 2).reshape(n, -1)  # [n][c][hy][wq]
+        s = torch.clamp(s, min=bound)
+        ref = (levels - 1) - (s.unsqueeze(-1) <= tab.view(1, 1, -1)).sum(-1)
+        assert torch.equal(idx.cpu().long(), ref.long())
+        assert torch.equal(idx2.cpu().long(), ref.long())
