@@ -501,6 +501,26 @@ def act(z, kind: int, slope: float = 0.0):
 
 
 # ------------------------------------------------------------------------------------------- norms
+def _count_direct_pair(ctx, gamma, beta) -> bool:
+    """A norm's (gamma, beta): both go to their direct gradient views (the backward kernel's accumulate mode,
+    no AccumulateGrad add per parameter) when both have one and both need a gradient; else neither does."""
+    nig = ctx.needs_input_grad
+    if nig[1] and nig[2] and direct_grad_view(gamma) is not None and direct_grad_view(beta) is not None:
+        count_direct_use(gamma, True)
+        count_direct_use(beta, True)
+        return True
+    return False
+
+
+def _param_grad_targets(ctx, gamma, beta, c: int, device):
+    """(dgamma, dbeta, accumulate) for a norm backward: the direct views (accumulate) or fresh tensors."""
+    if ctx.direct:
+        return direct_grad_view(gamma), direct_grad_view(beta), 1
+    if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+        return (torch.empty(c, dtype=torch.float32, device=device), torch.empty(c, dtype=torch.float32, device=device), 0)
+    return None, None, 0
+
+
 class GroupNormFn(torch.autograd.Function):
     """y = silu?(GroupNorm(x)) over NHWC x (GroupNorm32 / GroupNorm_leq32 / Normalize + SiLU)."""
 
@@ -516,6 +536,7 @@ class GroupNormFn(torch.autograd.Function):
              mr.data_ptr(), ab.data_ptr(), ws.data_ptr(), _dt(x), _sp())
         y = ops.group_norm_apply(x, ab, silu)
         ctx.groups, ctx.silu = groups, silu
+        ctx.direct = _count_direct_pair(ctx, gamma, beta)
         ctx.save_for_backward(x, gamma, beta, mr)
         return y
 
@@ -526,15 +547,17 @@ class GroupNormFn(torch.autograd.Function):
         n, h, w, c = x.shape
         hw = h * w
         dx = torch.empty((n, h, w, c), dtype=x.dtype, device=x.device)
-        want = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        dg = torch.empty(c, dtype=torch.float32, device=x.device) if want else None
-        dbt = torch.empty(c, dtype=torch.float32, device=x.device) if want else None
+        dg, dbt, acc = _param_grad_targets(ctx, gamma, beta, c, x.device)
         ws = torch.empty(int(_lib.load().rdeic_gn_train_ws_doubles(n, hw, c)), dtype=torch.float64, device=x.device)
         coef = torch.empty((n, ctx.groups, 2), dtype=torch.float32, device=x.device)
         call("rdeic_gn_train_bwd", x.data_ptr(), ops.pix_ld(x), dy.data_ptr(), c, n, hw, c, ctx.groups, mr.data_ptr(),
              gamma.data_ptr(), beta.data_ptr(), int(ctx.silu), dx.data_ptr(), c,
-             None if dg is None else dg.data_ptr(), None if dbt is None else dbt.data_ptr(), 0, ws.data_ptr(),
+             None if dg is None else dg.data_ptr(), None if dbt is None else dbt.data_ptr(), acc, ws.data_ptr(),
              coef.data_ptr(), _dt(x), _sp())
+        if ctx.direct:
+            notify_grad(gamma)
+            notify_grad(beta)
+            return dx, None, None, None, None, None
         return dx, dg, dbt, None, None, None
 
 
@@ -550,26 +573,29 @@ class LayerNormFn(torch.autograd.Function):
         call("rdeic_layernorm", x.data_ptr(), rows, c, x.stride(0), gamma.data_ptr(), beta.data_ptr(), float(eps),
              y.data_ptr(), c, _dt(x), _sp())
         ctx.eps = eps
-        ctx.save_for_backward(x, gamma)
+        ctx.direct = _count_direct_pair(ctx, gamma, beta)
+        ctx.save_for_backward(x, gamma, beta)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, gamma = ctx.saved_tensors
+        x, gamma, beta = ctx.saved_tensors
         dy = dy.contiguous()
         rows, c = x.shape
         dx = torch.empty((rows, c), dtype=x.dtype, device=x.device)
-        want = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
-        dg = db = ws = None
+        dg, db, acc = _param_grad_targets(ctx, gamma, beta, c, x.device)
+        ws = None
         nws = 0
-        if want:
-            dg = torch.empty(c, dtype=torch.float32, device=x.device)
-            db = torch.empty(c, dtype=torch.float32, device=x.device)
+        if dg is not None:
             nws = int(_lib.load().rdeic_layernorm_bwd_ws_floats(rows, c))
             ws = torch.empty(nws, dtype=torch.float32, device=x.device)
         call("rdeic_layernorm_bwd", x.data_ptr(), x.stride(0), rows, c, gamma.data_ptr(), float(ctx.eps), dy.data_ptr(),
-             c, dx.data_ptr(), c, None if dg is None else dg.data_ptr(), None if db is None else db.data_ptr(), 0,
+             c, dx.data_ptr(), c, None if dg is None else dg.data_ptr(), None if db is None else db.data_ptr(), acc,
              None if ws is None else ws.data_ptr(), nws, _dt(x), _sp())
+        if ctx.direct:
+            notify_grad(gamma)
+            notify_grad(beta)
+            return dx, None, None, None
         return dx, dg, db, None
 
 
