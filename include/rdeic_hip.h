@@ -449,11 +449,22 @@ int rdeic_gn_train_bwd(const void* x, int32_t ldx, const void* dy, int32_t ldy, 
                        int32_t groups, const float* mr, const float* gamma, const float* beta, int32_t silu, void* dx,
                        int32_t lddx, float* dgamma, float* dbeta, int32_t accumulate, double* ws, float* coef,
                        int32_t dtype, void* stream);
+/* the same with a second gradient of x added (dres [n*hw][ldr], null: none): dx = round(round(dx_gn) + dres), what
+ * autograd's sum of the two gradient tensors gives (the residual path of a block whose input feeds this norm) */
+int rdeic_gn_train_bwd_res(const void* x, int32_t ldx, const void* dy, int32_t ldy, int32_t n, int32_t hw, int32_t c,
+                           int32_t groups, const float* mr, const float* gamma, const float* beta, int32_t silu,
+                           const void* dres, int32_t ldr, void* dx, int32_t lddx, float* dgamma, float* dbeta,
+                           int32_t accumulate, double* ws, float* coef, int32_t dtype, void* stream);
 /* LayerNorm backward (statistics recomputed); dgamma / dbeta optional (ws then required) */
 size_t rdeic_layernorm_bwd_ws_floats(int64_t rows, int32_t c);
 int rdeic_layernorm_bwd(const void* x, int32_t ldx, int64_t rows, int32_t c, const float* gamma, float eps,
                         const void* dy, int32_t ldy, void* dx, int32_t lddx, float* dgamma, float* dbeta,
                         int32_t accumulate, float* ws, size_t ws_floats, int32_t dtype, void* stream);
+/* ... with a second gradient of x added (dres [rows][ldr], null: none), as rdeic_gn_train_bwd_res */
+int rdeic_layernorm_bwd_res(const void* x, int32_t ldx, int64_t rows, int32_t c, const float* gamma, float eps,
+                            const void* dy, int32_t ldy, const void* dres, int32_t ldr, void* dx, int32_t lddx,
+                            float* dgamma, float* dbeta, int32_t accumulate, float* ws, size_t ws_floats,
+                            int32_t dtype, void* stream);
 /* ds = p * (dp - rowsum(p * dp)) * scale  (p [rows][cols] of rdeic_softmax_rows, dp fp32) */
 int rdeic_softmax_bwd_rows(const void* p, const float* dp, int64_t rows, int32_t cols, float scale, void* ds,
                            int32_t dtype, void* stream);

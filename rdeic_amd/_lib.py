@@ -154,9 +154,13 @@ PROTOTYPES = {
     "rdeic_gn_train_fwd": (C.c_int, [_p, _i32, _i32, _i32, _i32, _i32, _f, _p, _p, _p, _p, _p, _i32, _p]),
     "rdeic_gn_train_bwd": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p, _i32, _p, _p,
                                      _i32, _p, _p, _i32, _p]),
+    "rdeic_gn_train_bwd_res": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p, _i32, _p,
+                                         _i32, _p, _p, _i32, _p, _p, _i32, _p]),
     "rdeic_layernorm_bwd_ws_floats": (_sz, [_i64, _i32]),
     "rdeic_layernorm_bwd": (C.c_int, [_p, _i32, _i64, _i32, _p, _f, _p, _i32, _p, _i32, _p, _p, _i32, _p, _sz, _i32,
                                       _p]),
+    "rdeic_layernorm_bwd_res": (C.c_int, [_p, _i32, _i64, _i32, _p, _f, _p, _i32, _p, _i32, _p, _i32, _p, _p, _i32, _p,
+                                          _sz, _i32, _p]),
     "rdeic_softmax_bwd_rows": (C.c_int, [_p, _p, _i64, _i32, _f, _p, _i32, _p]),
     "rdeic_geglu_bwd": (C.c_int, [_p, _i32, _i64, _i32, _p, _i32, _p, _i32, _i32, _p]),
     "rdeic_ckbd_train_anchor": (C.c_int, [_p, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _i32, _i32, _p]),

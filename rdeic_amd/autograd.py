@@ -521,11 +521,21 @@ def _param_grad_targets(ctx, gamma, beta, c: int, device):
     return None, None, 0
 
 
+def _res_grad(dxa, x):
+    """(pointer, row stride) of a passthrough alias's gradient (None: no gradient reached the alias)."""
+    if dxa is None:
+        return None, 0
+    if dxa.dtype != x.dtype or dxa.shape != x.shape:
+        raise ValueError("residual gradient must match the norm input")
+    dxa = dxa.contiguous()
+    return dxa.data_ptr(), dxa.shape[-1]
+
+
 class GroupNormFn(torch.autograd.Function):
     """y = silu?(GroupNorm(x)) over NHWC x (GroupNorm32 / GroupNorm_leq32 / Normalize + SiLU)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool):
+    def forward(ctx, x, gamma, beta, groups: int, eps: float, silu: bool, passthrough: bool = False):
         n, h, w, c = x.shape
         hw = h * w
         ld = ops.pix_ld(x)
@@ -538,10 +548,13 @@ class GroupNormFn(torch.autograd.Function):
         ctx.groups, ctx.silu = groups, silu
         ctx.direct = _count_direct_pair(ctx, gamma, beta)
         ctx.save_for_backward(x, gamma, beta, mr)
+        if passthrough:  # (y, x): x's other consumer takes the alias, its gradient comes back here (_res_grad)
+            ctx.set_materialize_grads(False)
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dxa=None):
         x, gamma, beta, mr = ctx.saved_tensors
         dy = dy.contiguous()
         n, h, w, c = x.shape
@@ -550,24 +563,27 @@ class GroupNormFn(torch.autograd.Function):
         dg, dbt, acc = _param_grad_targets(ctx, gamma, beta, c, x.device)
         ws = torch.empty(int(_lib.load().rdeic_gn_train_ws_doubles(n, hw, c)), dtype=torch.float64, device=x.device)
         coef = torch.empty((n, ctx.groups, 2), dtype=torch.float32, device=x.device)
-        call("rdeic_gn_train_bwd", x.data_ptr(), ops.pix_ld(x), dy.data_ptr(), c, n, hw, c, ctx.groups, mr.data_ptr(),
-             gamma.data_ptr(), beta.data_ptr(), int(ctx.silu), dx.data_ptr(), c,
+        dres, ldr = _res_grad(dxa, x)
+        call("rdeic_gn_train_bwd_res", x.data_ptr(), ops.pix_ld(x), dy.data_ptr(), c, n, hw, c, ctx.groups,
+             mr.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(ctx.silu), dres, ldr, dx.data_ptr(), c,
              None if dg is None else dg.data_ptr(), None if dbt is None else dbt.data_ptr(), acc, ws.data_ptr(),
              coef.data_ptr(), _dt(x), _sp())
         if ctx.direct:
             notify_grad(gamma)
             notify_grad(beta)
-            return dx, None, None, None, None, None
-        return dx, dg, dbt, None, None, None
+            return dx, None, None, None, None, None, None
+        return dx, dg, dbt, None, None, None, None
 
 
-def group_norm(x, gamma, beta, groups: int, eps: float, silu: bool):
-    return GroupNormFn.apply(x, gamma, beta, groups, eps, silu)
+def group_norm(x, gamma, beta, groups: int, eps: float, silu: bool, passthrough: bool = False):
+    """passthrough: also return an alias of x for x's second consumer (a residual / skip path); that consumer's
+    gradient is then added inside this norm's backward kernel instead of by an autograd add launch."""
+    return GroupNormFn.apply(x, gamma, beta, groups, eps, silu, passthrough)
 
 
 class LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps: float):
+    def forward(ctx, x, gamma, beta, eps: float, passthrough: bool = False):
         rows, c = x.shape
         y = torch.empty((rows, c), dtype=x.dtype, device=x.device)
         call("rdeic_layernorm", x.data_ptr(), rows, c, x.stride(0), gamma.data_ptr(), beta.data_ptr(), float(eps),
@@ -575,10 +591,13 @@ class LayerNormFn(torch.autograd.Function):
         ctx.eps = eps
         ctx.direct = _count_direct_pair(ctx, gamma, beta)
         ctx.save_for_backward(x, gamma, beta)
+        if passthrough:
+            ctx.set_materialize_grads(False)
+            return y, x.view_as(x)
         return y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dxa=None):
         x, gamma, beta = ctx.saved_tensors
         dy = dy.contiguous()
         rows, c = x.shape
@@ -589,18 +608,20 @@ class LayerNormFn(torch.autograd.Function):
         if dg is not None:
             nws = int(_lib.load().rdeic_layernorm_bwd_ws_floats(rows, c))
             ws = torch.empty(nws, dtype=torch.float32, device=x.device)
-        call("rdeic_layernorm_bwd", x.data_ptr(), x.stride(0), rows, c, gamma.data_ptr(), float(ctx.eps), dy.data_ptr(),
-             c, dx.data_ptr(), c, None if dg is None else dg.data_ptr(), None if db is None else db.data_ptr(), acc,
-             None if ws is None else ws.data_ptr(), nws, _dt(x), _sp())
+        dres, ldr = _res_grad(dxa, x)
+        call("rdeic_layernorm_bwd_res", x.data_ptr(), x.stride(0), rows, c, gamma.data_ptr(), float(ctx.eps),
+             dy.data_ptr(), c, dres, ldr, dx.data_ptr(), c, None if dg is None else dg.data_ptr(),
+             None if db is None else db.data_ptr(), acc, None if ws is None else ws.data_ptr(), nws, _dt(x), _sp())
         if ctx.direct:
             notify_grad(gamma)
             notify_grad(beta)
-            return dx, None, None, None
-        return dx, dg, db, None
+            return dx, None, None, None, None
+        return dx, dg, db, None, None
 
 
-def layer_norm(x, gamma, beta, eps: float = 1e-5):
-    return LayerNormFn.apply(x, gamma, beta, eps)
+def layer_norm(x, gamma, beta, eps: float = 1e-5, passthrough: bool = False):
+    """passthrough: as group_norm's (the transformer's residual around each LayerNorm)."""
+    return LayerNormFn.apply(x, gamma, beta, eps, passthrough)
 
 
 # --------------------------------------------------------------------------------------- attention

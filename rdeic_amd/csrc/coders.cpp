@@ -464,7 +464,7 @@ extern "C" {
 int rdeic_version(void) { return 1; }
 
 // number of entry points declared in include/rdeic_hip.h (checked by tests/test_abi.py)
-int rdeic_abi_count(void) { return 91; }
+int rdeic_abi_count(void) { return 93; }
 
 static int pmf_to_quantized_cdf_impl(const float* pmf, int32_t n, int32_t precision, uint32_t* cdf_out) {
   if (!pmf || !cdf_out || n <= 0 || precision <= 0 || precision > 24) return RDEIC_EINVAL;

@@ -657,7 +657,7 @@ template <typename T>
 __global__ void gnt_bwd_dx_kernel(const T* __restrict__ x, int ldx, const T* __restrict__ dy, int ldy, int n, int hw,
                                   int c, int groups, const float* __restrict__ mr, const float* __restrict__ coef,
                                   const float* __restrict__ gamma, const float* __restrict__ beta, int silu,
-                                  T* __restrict__ dx, int lddx) {
+                                  T* __restrict__ dx, int lddx, const T* __restrict__ dres, int ldr) {
   const long total = (long)n * hw * c;
   const int cpg = c / groups;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -674,7 +674,10 @@ __global__ void gnt_bwd_dx_kernel(const T* __restrict__ x, int ldx, const T* __r
       const float s = 1.f / (1.f + expf(-u));
       d *= s * (1.f + u * (1.f - s));
     }
-    dx[pix * lddx + ch] = from_f32<T>(rstd * (ga * d - coef[gi] - xh * coef[gi + 1]));
+    const float v = rstd * (ga * d - coef[gi] - xh * coef[gi + 1]);
+    // dres: a second gradient of x (a residual path), added as autograd would add the two tensors: each
+    // rounded to T first, then summed in fp32 and rounded again
+    dx[pix * lddx + ch] = dres ? from_f32<T>(to_f32(from_f32<T>(v)) + to_f32(dres[pix * ldr + ch])) : from_f32<T>(v);
   }
 }
 
@@ -698,7 +701,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ x, int ldx, long rows, int c,
                                                             const float* __restrict__ gamma, float eps,
                                                             const T* __restrict__ dy, int ldy, T* __restrict__ dx,
-                                                            int lddx, float* __restrict__ dgb_part) {
+                                                            int lddx, float* __restrict__ dgb_part,
+                                                            const T* __restrict__ dres, int ldr) {
   constexpr int MAXJ = 32;
   const int lane = threadIdx.x & 63;
   const long wv = blockIdx.x * 4L + (threadIdx.x >> 6);
@@ -748,7 +752,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict_
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
       const int col = lane + 64 * j;
-      if (j < nj && col < c) dx[r * lddx + col] = from_f32<T>(rstd * (gv[j] - m1 - xv[j] * m2));
+      if (j < nj && col < c) {
+        const float v = rstd * (gv[j] - m1 - xv[j] * m2);  // + dres as autograd's add of the two T tensors
+        dx[r * lddx + col] = dres ? from_f32<T>(to_f32(from_f32<T>(v)) + to_f32(dres[r * ldr + col])) : from_f32<T>(v);
+      }
     }
   }
   if (dgb_part) {
@@ -1315,6 +1322,15 @@ extern "C" int rdeic_gn_train_bwd(const void* x, int32_t ldx, const void* dy, in
                                   int32_t c, int32_t groups, const float* mr, const float* gamma, const float* beta,
                                   int32_t silu, void* dx, int32_t lddx, float* dgamma, float* dbeta,
                                   int32_t accumulate, double* ws, float* coef, int32_t dtype, void* stream) {
+  return rdeic_gn_train_bwd_res(x, ldx, dy, ldy, n, hw, c, groups, mr, gamma, beta, silu, nullptr, 0, dx, lddx, dgamma,
+                                dbeta, accumulate, ws, coef, dtype, stream);
+}
+
+extern "C" int rdeic_gn_train_bwd_res(const void* x, int32_t ldx, const void* dy, int32_t ldy, int32_t n, int32_t hw,
+                                      int32_t c, int32_t groups, const float* mr, const float* gamma, const float* beta,
+                                      int32_t silu, const void* dres, int32_t ldr, void* dx, int32_t lddx,
+                                      float* dgamma, float* dbeta, int32_t accumulate, double* ws, float* coef,
+                                      int32_t dtype, void* stream) {
   if (!x || !dy || !dx || !mr || !ws || !coef || n <= 0 || hw <= 0 || c <= 0 || groups <= 0 || c % groups)
     return RDEIC_EINVAL;
   hipStream_t s = (hipStream_t)stream;
@@ -1332,10 +1348,10 @@ extern "C" int rdeic_gn_train_bwd(const void* x, int32_t ldx, const void* dy, in
   const int g = grid_1d((long)n * hw * c);
   if (dtype == 1)
     hipLaunchKernelGGL(gnt_bwd_dx_kernel<bf16>, dim3(g), dim3(256), 0, s, (const bf16*)x, ldx, (const bf16*)dy, ldy,
-                       n, hw, c, groups, mr, coef, gamma, beta, silu, (bf16*)dx, lddx);
+                       n, hw, c, groups, mr, coef, gamma, beta, silu, (bf16*)dx, lddx, (const bf16*)dres, ldr);
   else
     hipLaunchKernelGGL(gnt_bwd_dx_kernel<float>, dim3(g), dim3(256), 0, s, (const float*)x, ldx, (const float*)dy,
-                       ldy, n, hw, c, groups, mr, coef, gamma, beta, silu, (float*)dx, lddx);
+                       ldy, n, hw, c, groups, mr, coef, gamma, beta, silu, (float*)dx, lddx, (const float*)dres, ldr);
   if (dgamma || dbeta)
     hipLaunchKernelGGL(gnt_param_grad_kernel, dim3((c + 255) / 256), dim3(256), 0, s, nc, n, c, dgamma, dbeta,
                        accumulate);
@@ -1353,6 +1369,14 @@ extern "C" size_t rdeic_layernorm_bwd_ws_floats(int64_t rows, int32_t c) {
 extern "C" int rdeic_layernorm_bwd(const void* x, int32_t ldx, int64_t rows, int32_t c, const float* gamma, float eps,
                                    const void* dy, int32_t ldy, void* dx, int32_t lddx, float* dgamma, float* dbeta,
                                    int32_t accumulate, float* ws, size_t ws_floats, int32_t dtype, void* stream) {
+  return rdeic_layernorm_bwd_res(x, ldx, rows, c, gamma, eps, dy, ldy, nullptr, 0, dx, lddx, dgamma, dbeta, accumulate,
+                                 ws, ws_floats, dtype, stream);
+}
+
+extern "C" int rdeic_layernorm_bwd_res(const void* x, int32_t ldx, int64_t rows, int32_t c, const float* gamma,
+                                       float eps, const void* dy, int32_t ldy, const void* dres, int32_t ldr, void* dx,
+                                       int32_t lddx, float* dgamma, float* dbeta, int32_t accumulate, float* ws,
+                                       size_t ws_floats, int32_t dtype, void* stream) {
   if (!x || !dy || !dx || !gamma || rows <= 0 || c <= 0 || c > 2048) return RDEIC_EINVAL;
   const bool pg = dgamma && dbeta;
   if (pg && (!ws || ws_floats < rdeic_layernorm_bwd_ws_floats(rows, c))) return RDEIC_ENOSPC;
@@ -1360,10 +1384,10 @@ extern "C" int rdeic_layernorm_bwd(const void* x, int32_t ldx, int64_t rows, int
   const int blocks = (int)ln_bwd_blocks(rows);
   if (dtype == 1)
     hipLaunchKernelGGL(layernorm_bwd_kernel<bf16>, dim3(blocks), dim3(256), 0, s, (const bf16*)x, ldx, (long)rows, c,
-                       gamma, eps, (const bf16*)dy, ldy, (bf16*)dx, lddx, pg ? ws : nullptr);
+                       gamma, eps, (const bf16*)dy, ldy, (bf16*)dx, lddx, pg ? ws : nullptr, (const bf16*)dres, ldr);
   else
     hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)x, ldx, (long)rows, c,
-                       gamma, eps, (const float*)dy, ldy, (float*)dx, lddx, pg ? ws : nullptr);
+                       gamma, eps, (const float*)dy, ldy, (float*)dx, lddx, pg ? ws : nullptr, (const float*)dres, ldr);
   if (pg) {
     const long nw = (long)blocks * 4;
     const int nchunk = (int)((nw + LN_CHUNK - 1) / LN_CHUNK);

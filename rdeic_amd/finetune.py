@@ -145,11 +145,11 @@ class FineTuner:
         b = self.m.store.t.get(prefix + ".bias")
         return AG.linear(x, w, b, res=res, key=None if w.requires_grad else prefix, out_f32=out_f32)
 
-    def gn(self, x, prefix, groups, eps, silu):
-        return AG.group_norm(x, self.p(prefix + ".weight"), self.p(prefix + ".bias"), groups, eps, silu)
+    def gn(self, x, prefix, groups, eps, silu, passthrough=False):
+        return AG.group_norm(x, self.p(prefix + ".weight"), self.p(prefix + ".bias"), groups, eps, silu, passthrough)
 
-    def ln(self, x, prefix):
-        return AG.layer_norm(x, self.p(prefix + ".weight"), self.p(prefix + ".bias"), 1e-5)
+    def ln(self, x, prefix, passthrough=False):
+        return AG.layer_norm(x, self.p(prefix + ".weight"), self.p(prefix + ".bias"), 1e-5, passthrough)
 
     # ------------------------------------------------------------------ UNet / control (openaimodel.py, rdeic.py)
     def time_embed(self, net, temb):
@@ -160,11 +160,13 @@ class FineTuner:
 
     def resblock(self, rb: ResBlock, x, semb):
         """openaimodel.py:254-274 / rdeic.py:566-598 (emb_layers Linear, no scale-shift norm)."""
-        h = self.gn(x, rb.prefix + ".in_layers.0", rb.gn_in, 1e-5, True)
+        # x feeds the first norm and the skip path: the skip path takes the norm's passthrough alias, so its
+        # gradient is added inside the norm's backward kernel (no autograd add launch)
+        h, xs = self.gn(x, rb.prefix + ".in_layers.0", rb.gn_in, 1e-5, True, passthrough=True)
         emb = self.linear(semb, rb.prefix + ".emb_layers.1")
         h = self.conv(h, rb.prefix + ".in_layers.2", emb=emb)
         h = self.gn(h, rb.prefix + ".out_layers.0", rb.gn_out, 1e-5, True)
-        skip = x if rb.cin == rb.cout else self.conv(x, rb.prefix + ".skip_connection")
+        skip = xs if rb.cin == rb.cout else self.conv(xs, rb.prefix + ".skip_connection")
         return self.conv(h, rb.prefix + ".out_layers.3", res=skip)
 
     def transformer(self, t: SpatialTransformer, x, ctx_rows, batch):
@@ -172,25 +174,26 @@ class FineTuner:
         B, H, W_, C = x.shape
         L = H * W_
         tb = t.prefix + ".transformer_blocks.0"
-        h = self.gn(x, t.prefix + ".norm", t.gn, 1e-6, False)
+        # every residual input also feeds a norm: the residual takes the norm's passthrough alias (see resblock)
+        h, xs = self.gn(x, t.prefix + ".norm", t.gn, 1e-6, False, passthrough=True)
         h = self.linear(h.reshape(B * L, C), t.prefix + ".proj_in")
         scale = t.dh ** -0.5
-        n1 = self.ln(h, tb + ".norm1")
+        n1, hs = self.ln(h, tb + ".norm1", passthrough=True)
         q = self.linear(n1, tb + ".attn1.to_q")
         k = self.linear(n1, tb + ".attn1.to_k")
         v = self.linear(n1, tb + ".attn1.to_v")
         o = AG.attention(q, k, v, batch, t.heads, scale)
-        h = self.linear(o, tb + ".attn1.to_out.0", res=h)
-        n2 = self.ln(h, tb + ".norm2")
+        h = self.linear(o, tb + ".attn1.to_out.0", res=hs)
+        n2, hs = self.ln(h, tb + ".norm2", passthrough=True)
         q = self.linear(n2, tb + ".attn2.to_q")
         k = self.linear(ctx_rows, tb + ".attn2.to_k")
         v = self.linear(ctx_rows, tb + ".attn2.to_v")
         o = AG.attention(q, k, v, batch, t.heads, scale)
-        h = self.linear(o, tb + ".attn2.to_out.0", res=h)
-        n3 = self.ln(h, tb + ".norm3")
+        h = self.linear(o, tb + ".attn2.to_out.0", res=hs)
+        n3, hs = self.ln(h, tb + ".norm3", passthrough=True)
         g = AG.geglu(self.linear(n3, tb + ".ff.net.0.proj"))
-        h = self.linear(g, tb + ".ff.net.2", res=h)
-        out = self.linear(h, t.prefix + ".proj_out", res=x.reshape(B * L, C))
+        h = self.linear(g, tb + ".ff.net.2", res=hs)
+        out = self.linear(h, t.prefix + ".proj_out", res=xs.reshape(B * L, C))
         return out.view(B, H, W_, C)
 
     def run_layers(self, net, layers, x, semb, ctx_rows, batch):
