@@ -38,6 +38,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--splitk-train", default=None, metavar="KDIV,MAX,TARGET",
+                    help="split counts of the step's >= 32 k-tile convs (A/B; ops.SPLITK_TRAIN)")
     ap.add_argument("--ft-splitk", default="short", choices=["short", "long", "off"],
                     help="split-K policy of the step's convs (A/B; finetune.FT_SPLITK)")
     ap.add_argument("--eager", action="store_true",
@@ -53,6 +55,8 @@ def main(argv=None):
     from rdeic_amd import finetune
     from rdeic_amd.finetune import CapturedStep, FineTuner, nchw_draws_to_nhwc
     finetune.FT_SPLITK = args.ft_splitk
+    if args.splitk_train:
+        ops.SPLITK_TRAIN = tuple(int(v) for v in args.splitk_train.split(","))
     from rdeic_amd.rdeic import RDEIC
     from rdeic_amd.synthetic import synth_context, synth_image, train_draws
 

@@ -334,6 +334,9 @@ def splitk_state():
 # batch (bench, CLI --batch_size / --micro_batch_size, data-parallel shards). Training (short_k,
 # B=1) sizes splits from the real M: it needs no batch invariance.
 SPLITK_NOMINAL_BATCH = 16
+# Training (short_k) split counts for the >= 32 k-tile layers: None = the inference rule below; else
+# (k-tiles per split at least, max splits, target blocks) -- an A/B knob (bench_train.py --splitk-train)
+SPLITK_TRAIN = None
 # bf16 entropy model (Compression nets at the y / z resolution): split-K allowed, per-image counts
 SPLITK_ENTROPY = True
 
@@ -397,6 +400,9 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
     nk = -(-(p.kh * p.kw * p.cin) // 64)
     if short and tiles < 128 and 8 <= nk < 32:
         return max(1, min(-(-512 // tiles), nk // 4, 8))
+    if short and SPLITK_TRAIN is not None and tiles < 192 and nk >= 32:  # A/B knob (bench_train.py --splitk-train)
+        kdiv, smax, target = SPLITK_TRAIN
+        return max(1, min(-(-target // tiles), nk // kdiv, smax))
     if tiles >= 192 or nk < 32:
         return 1
     # tiles x splits within the 512 co-resident 128x128 blocks (2 per CU): one more split past that
