@@ -79,6 +79,8 @@ def parse(argv=None):
     ap.add_argument("--streams", type=int, default=5,
                     help="codec sessions in flight per GPU (host thread + HIP stream each; RDEIC.session): one "
                          "batch's host rANS coding and small entropy-stage kernels overlap another batch's GPU work")
+    ap.add_argument("--splitk-rule", default=None, metavar="BLOCKS,MAX",
+                    help="inference split-K rule of the small-M convs (A/B only; ops.SPLITK_BLOCKS / SPLITK_MAX)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--prof-every", type=int, default=8,
@@ -160,6 +162,8 @@ def main():
     for kv in args.conv_option:
         k, v = kv.split("=")
         ops.set_conv_option(int(k), int(v))
+    if args.splitk_rule:
+        ops.SPLITK_BLOCKS, ops.SPLITK_MAX = (int(v) for v in args.splitk_rule.split(","))
 
     imgs = torch.from_numpy(np.stack([synth_image(S, S, 231 + g) for g in range(g0, g1)])).to(dev)
     draws = [relay_noise((1, 4, S // 8, S // 8), 231 + g, args.ddim_steps) for g in range(g0, g1)]

@@ -334,6 +334,10 @@ def splitk_state():
 # batch (bench, CLI --batch_size / --micro_batch_size, data-parallel shards). Training (short_k,
 # B=1) sizes splits from the real M: it needs no batch invariance.
 SPLITK_NOMINAL_BATCH = 16
+# Inference split rule: tiles x splits within SPLITK_BLOCKS co-resident 128x128 blocks, at most SPLITK_MAX splits
+# (A/B knobs: bench.py --splitk-rule BLOCKS,MAX; a change moves the k grouping and so the bf16 rounding of the
+# split layers, the entropy nets' too: both codec sides apply the same rule, so bitstreams stay self-consistent)
+SPLITK_BLOCKS, SPLITK_MAX = 512, 8
 # Training (short_k) split counts for the >= 32 k-tile layers: None = the inference rule below; else
 # (k-tiles per split at least, max splits, target blocks) -- an A/B knob (bench_train.py --splitk-train)
 SPLITK_TRAIN = None
@@ -408,7 +412,7 @@ def _splitk_count(x, x2, M: int, p: "ConvParams", fused: bool, out: torch.Tensor
     # tiles x splits within the 512 co-resident 128x128 blocks (2 per CU): one more split past that
     # starts a second round of blocks (tools/splitk_bench.py, UNet 8x8 level: 7 splits 419 / 503 TF,
     # 6 splits 528 / 674 TF for the 1280 / 2560-channel inputs)
-    return max(1, min(512 // tiles, nk // 16, 8))
+    return max(1, min(SPLITK_BLOCKS // tiles, nk // 16, SPLITK_MAX))
 
 
 _SPLITK_KEEP: list = []  # every workspace ever handed out: recorded launch plans hold their pointers

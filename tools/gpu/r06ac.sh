@@ -1,0 +1,13 @@
+#!/bin/bash
+# r06: inference split-K rule A/B in the concurrent bench (driver counts), alternating on one box.
+set -o pipefail
+TAG=${1:-r06ac}
+O=$PWD/gpurun_out/$TAG
+mkdir -p $O
+for rep in 1 2 3; do
+  for v in base 512,4 768,8 1024,8; do
+    A=""; [ $v != base ] && A="--splitk-rule $v"
+    timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --fp32-steps 0 $A > $O/${v}_$rep.json 2> $O/${v}_$rep.err || { echo "bench $v failed"; tail -5 $O/${v}_$rep.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/${v}_$rep.json').read().strip().splitlines()[-1]); print('$v $rep', d['value'], d['ms_per_step'], d['roofline']['frac'], d['config']['mean_bpp'])"
+  done
+done
