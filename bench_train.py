@@ -38,6 +38,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--bucket-mb", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--conv-option", action="append", default=[], metavar="KEY=VALUE",
+                    help="rdeic_set_conv_option(KEY, VALUE) before the run (A/B only)")
     ap.add_argument("--splitk-train", default=None, metavar="KDIV,MAX,TARGET",
                     help="split counts of the step's >= 32 k-tile convs (A/B; ops.SPLITK_TRAIN)")
     ap.add_argument("--ft-splitk", default="short", choices=["short", "long", "off"],
@@ -55,6 +57,9 @@ def main(argv=None):
     from rdeic_amd import finetune
     from rdeic_amd.finetune import CapturedStep, FineTuner, nchw_draws_to_nhwc
     finetune.FT_SPLITK = args.ft_splitk
+    for kv in args.conv_option:
+        k, v = kv.split("=")
+        ops.set_conv_option(int(k), int(v))
     if args.splitk_train:
         ops.SPLITK_TRAIN = tuple(int(v) for v in args.splitk_train.split(","))
     from rdeic_amd.rdeic import RDEIC
